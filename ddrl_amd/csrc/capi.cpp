@@ -1,0 +1,572 @@
+// C-ABI of libddrl_hip.so (declared in include/ddrl_hip.h).
+// Owns every device buffer of a training shard; all work is enqueued on one HIP stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ddrl_hip.h"
+#include "kernels.h"
+
+namespace {
+thread_local std::string g_err;
+
+int fail(const std::string& msg) {
+  g_err = msg;
+  return -1;
+}
+
+#define HIPCHK(x)                                                                   \
+  do {                                                                              \
+    hipError_t e_ = (x);                                                            \
+    if (e_ != hipSuccess)                                                           \
+      return fail(std::string(#x) + ": " + hipGetErrorString(e_));                  \
+  } while (0)
+
+#define CHK_CTX(c) \
+  if (!(c)) return fail("null context")
+
+int ffn_param_count(int d, int A) { return d * 64 * 2 + 128 + 2 * 4096 + 128 + 64 * 2 * A + 2 * A + 65; }
+int gnn_param_count(int A) {
+  const int net = 4 * 1216 + 1216 + 2 * 4096;
+  return net + 64 * 2 * A + 2 * A + net + 64 + 1;
+}
+
+struct Policy {
+  int k = 0, d = 0, C = 0, n_params = 0, R = 0, nb = 0;
+  int agents[DDRL_MAXAG] = {0};
+  RecLayout lay{};
+  float *theta = nullptr, *m = nullptr, *v = nullptr, *beta_pow = nullptr;
+  float *rec = nullptr, *stage = nullptr, *last_v = nullptr, *adv_norm = nullptr;
+  float *stats = nullptr, *grad = nullptr;
+  double* partials = nullptr;
+  int last_steps = 0;
+};
+}  // namespace
+
+struct ddrl_ctx {
+  ddrl_cfg cfg{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  Policy pol[DDRL_MAXP];
+  RouteArgs route{};
+  double *f_n = nullptr, *f_M = nullptr, *f_S = nullptr, *f_normc = nullptr;
+  uint8_t* done_tn = nullptr;
+  float** stage_tab = nullptr;    // device array of per-policy stage pointers
+  int32_t* zero_perm = nullptr;
+  UpdateArgs* d_uargs = nullptr;  // device copy of the per-workgroup update arguments
+  // host-variant staging
+  float *h_obs = nullptr, *h_eps = nullptr, *h_act = nullptr;
+  std::vector<void*> allocs;
+};
+
+template <class T>
+static int dalloc(ddrl_ctx* c, T** p, size_t count) {
+  void* ptr = nullptr;
+  const size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+  hipError_t e = hipMalloc(&ptr, bytes);
+  if (e != hipSuccess) return fail(std::string("hipMalloc failed: ") + hipGetErrorString(e));
+  e = hipMemset(ptr, 0, bytes);
+  if (e != hipSuccess) return fail(std::string("hipMemset failed: ") + hipGetErrorString(e));
+  c->allocs.push_back(ptr);
+  *p = static_cast<T*>(ptr);
+  return 0;
+}
+
+static RecLayout make_layout(const ddrl_cfg& cfg, int d) {
+  RecLayout L;
+  const int A = cfg.act_dim;
+  L.obs = 0;
+  const int obs_len = cfg.model_kind == DDRL_MODEL_GNN ? 4 * 23 + 1 : d;
+  L.act = obs_len;
+  L.logit = L.act + A;
+  L.logp = L.logit + 2 * A;
+  L.vf = L.logp + 1;
+  L.adv = L.vf + 1;
+  L.vt = L.adv + 1;
+  L.rew = L.vt + 1;
+  L.stride = (L.rew + 1 + 3) & ~3;
+  return L;
+}
+
+static int validate(const ddrl_cfg& c) {
+  if (c.n_envs <= 0 || c.frag_len <= 0) return fail("n_envs and frag_len must be positive");
+  if (c.n_policies < 1 || c.n_policies > DDRL_MAXP) return fail("n_policies must be in [1, 4]");
+  if (c.n_agents < 1 || c.n_agents > DDRL_MAXAG) return fail("n_agents must be in [1, 4]");
+  if (c.act_dim != 2 && c.act_dim != 4 && c.act_dim != 8) return fail("act_dim must be 2, 4 or 8");
+  if (c.obs_full_dim < 1 || c.obs_full_dim > DDRL_MAXFULL) return fail("obs_full_dim out of range");
+  if (c.sgd_minibatch_size != 128) return fail("sgd_minibatch_size must be 128 (fused kernel tile)");
+  if (c.num_sgd_iter < 1) return fail("num_sgd_iter must be >= 1");
+  for (int j = 0; j < c.n_agents; ++j)
+    if (c.agent_policy[j] < 0 || c.agent_policy[j] >= c.n_policies) return fail("bad agent_policy");
+  for (int p = 0; p < c.n_policies; ++p) {
+    const int d = c.obs_dim[p];
+    if (d < 1 || d > DDRL_MAX_OBS) return fail("obs_dim out of range");
+    if (c.model_kind == DDRL_MODEL_FFN && d > 48) return fail("ffn obs_dim must be <= 48");
+  }
+  if (c.model_kind == DDRL_MODEL_GNN && (c.n_policies != 1 || c.n_agents != 4 || c.obs_dim[0] != 19))
+    return fail("gnn requires one shared leg policy, 4 agents and 19 features per node");
+  for (int j = 0; j < c.n_agents; ++j) {
+    const int d = c.obs_dim[c.agent_policy[j]];
+    for (int f = 0; f < d; ++f)
+      if (c.obs_index[j][f] < 0 || c.obs_index[j][f] >= c.obs_full_dim) return fail("bad obs_index");
+    if (c.n_contact[j] < 0 || c.n_contact[j] > 14) return fail("bad n_contact");
+    for (int b = 0; b < c.n_contact[j]; ++b)
+      if (c.contact_index[j][b] < 0 || c.contact_index[j][b] >= 14) return fail("bad contact_index");
+    for (int a = 0; a < c.act_dim; ++a)
+      if (c.act_index[j][a] < 0 || c.act_index[j][a] >= 8) return fail("bad act_index");
+  }
+  return 0;
+}
+
+extern "C" {
+
+int ddrl_abi_version(void) { return DDRL_ABI_VERSION; }
+const char* ddrl_last_error(void) { return g_err.c_str(); }
+
+int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
+  if (!cfg || !out) return fail("null argument");
+  if (validate(*cfg)) return -1;
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail("device index out of range");
+  HIPCHK(hipSetDevice(device));
+  ddrl_ctx* c = new ddrl_ctx();
+  c->cfg = *cfg;
+  c->device = device;
+  const ddrl_cfg& g = c->cfg;
+  const int N = g.n_envs, T = g.frag_len;
+  RouteArgs& ra = c->route;
+  ra.P = g.n_policies; ra.N = N; ra.A = g.act_dim; ra.full_dim = g.obs_full_dim;
+  ra.n_agents = g.n_agents; ra.model = g.model_kind;
+  for (int j = 0; j < 4; ++j) ra.leg_angle[j] = g.leg_angle_deg[j];
+  int rc = 0;
+  for (int p = 0; p < g.n_policies && !rc; ++p) {
+    Policy& P = c->pol[p];
+    P.d = g.obs_dim[p];
+    for (int j = 0; j < g.n_agents; ++j)
+      if (g.agent_policy[j] == p) P.agents[P.k++] = j;
+    if (P.k == 0) { rc = fail("policy without agents"); break; }
+    P.C = N * P.k;
+    P.R = T * P.C;
+    P.nb = std::max(1, P.R / g.sgd_minibatch_size);
+    P.lay = make_layout(g, P.d);
+    P.n_params = g.model_kind == DDRL_MODEL_FFN ? ffn_param_count(P.d, g.act_dim) : gnn_param_count(g.act_dim);
+    PolicyRoute& pr = ra.pol[p];
+    pr.k = P.k; pr.d = P.d;
+    for (int s = 0; s < P.k; ++s) {
+      pr.agent[s] = P.agents[s];
+      for (int f = 0; f < DDRL_MAXD; ++f) pr.obs_index[s][f] = g.obs_index[P.agents[s]][f];
+      for (int a = 0; a < 8; ++a) pr.act_index[s][a] = g.act_index[P.agents[s]][a];
+    }
+    const size_t stage_n = g.model_kind == DDRL_MODEL_GNN ? (size_t)N * 4 * 23 : (size_t)P.C * P.d;
+    rc = rc || dalloc(c, &P.theta, P.n_params) || dalloc(c, &P.m, P.n_params) ||
+         dalloc(c, &P.v, P.n_params) || dalloc(c, &P.beta_pow, 2) || dalloc(c, &P.grad, P.n_params) ||
+         dalloc(c, &P.rec, (size_t)P.R * P.lay.stride) || dalloc(c, &P.stage, stage_n) ||
+         dalloc(c, &P.last_v, P.C) || dalloc(c, &P.adv_norm, 2) ||
+         dalloc(c, &P.partials, 2 * (size_t)((P.C + 255) / 256)) ||
+         dalloc(c, &P.stats, (size_t)g.num_sgd_iter * P.nb * 8);
+    if (!rc) {
+      float bp[2] = {g.adam_beta1, g.adam_beta2};
+      if (hipMemcpy(P.beta_pow, bp, sizeof(bp), hipMemcpyHostToDevice) != hipSuccess) rc = fail("init beta_pow");
+      float an[2] = {0.f, 1.f};
+      if (hipMemcpy(P.adv_norm, an, sizeof(an), hipMemcpyHostToDevice) != hipSuccess) rc = fail("init adv_norm");
+    }
+  }
+  rc = rc || dalloc(c, &c->f_n, 1) || dalloc(c, &c->f_M, DDRL_MAXFULL) || dalloc(c, &c->f_S, DDRL_MAXFULL) ||
+       dalloc(c, &c->f_normc, 2 * DDRL_MAXFULL) || dalloc(c, &c->done_tn, (size_t)T * N) ||
+       dalloc(c, &c->stage_tab, DDRL_MAXP) || dalloc(c, &c->zero_perm, 4) ||
+       dalloc(c, &c->d_uargs, DDRL_MAXP) ||
+       dalloc(c, &c->h_obs, (size_t)N * g.obs_full_dim) ||
+       dalloc(c, &c->h_eps, (size_t)N * g.n_agents * g.act_dim) || dalloc(c, &c->h_act, (size_t)N * 8);
+  if (!rc) {
+    float* tab[DDRL_MAXP] = {nullptr};
+    for (int p = 0; p < g.n_policies; ++p) tab[p] = c->pol[p].stage;
+    if (hipMemcpy(c->stage_tab, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess) rc = fail("stage table");
+  }
+  if (!rc && hipDeviceSynchronize() != hipSuccess) rc = fail("device sync after init");
+  if (rc) {
+    ddrl_ctx_destroy(c);
+    return -1;
+  }
+  *out = c;
+  return 0;
+}
+
+int ddrl_ctx_destroy(ddrl_ctx* c) {
+  if (!c) return 0;
+  (void)hipSetDevice(c->device);
+  (void)hipDeviceSynchronize();
+  for (void* p : c->allocs) (void)hipFree(p);
+  delete c;
+  return 0;
+}
+
+int ddrl_set_stream(ddrl_ctx* c, void* s) {
+  CHK_CTX(c);
+  c->stream = static_cast<hipStream_t>(s);
+  return 0;
+}
+
+int ddrl_synchronize(ddrl_ctx* c) {
+  CHK_CTX(c);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int ddrl_param_count(ddrl_ctx* c, int pid, int64_t* n) {
+  CHK_CTX(c);
+  if (pid < 0 || pid >= c->cfg.n_policies || !n) return fail("bad policy id");
+  *n = c->pol[pid].n_params;
+  return 0;
+}
+
+int ddrl_record_layout(ddrl_ctx* c, int pid, int32_t* o) {
+  CHK_CTX(c);
+  if (pid < 0 || pid >= c->cfg.n_policies || !o) return fail("bad policy id");
+  const RecLayout& L = c->pol[pid].lay;
+  o[0] = L.stride; o[1] = L.obs; o[2] = L.act; o[3] = L.logit; o[4] = L.logp;
+  o[5] = L.vf; o[6] = L.adv; o[7] = L.vt; o[8] = L.rew; o[9] = c->pol[pid].C;
+  return 0;
+}
+
+static int check_n(ddrl_ctx* c, int pid, size_t n) {
+  if (!c) return fail("null context");
+  if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
+  if (n != (size_t)c->pol[pid].n_params) return fail("parameter count mismatch");
+  return 0;
+}
+
+int ddrl_params_set(ddrl_ctx* c, int pid, const float* h, size_t n) {
+  if (check_n(c, pid, n)) return -1;
+  HIPCHK(hipMemcpyAsync(c->pol[pid].theta, h, n * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int ddrl_params_get(ddrl_ctx* c, int pid, float* h, size_t n) {
+  if (check_n(c, pid, n)) return -1;
+  HIPCHK(hipMemcpyAsync(h, c->pol[pid].theta, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int ddrl_adam_set(ddrl_ctx* c, int pid, const float* m, const float* v, size_t n, float b1p, float b2p) {
+  if (check_n(c, pid, n)) return -1;
+  Policy& P = c->pol[pid];
+  HIPCHK(hipMemcpyAsync(P.m, m, n * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(P.v, v, n * 4, hipMemcpyHostToDevice, c->stream));
+  float bp[2] = {b1p, b2p};
+  HIPCHK(hipMemcpyAsync(P.beta_pow, bp, 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int ddrl_adam_get(ddrl_ctx* c, int pid, float* m, float* v, size_t n, float* b1p, float* b2p) {
+  if (check_n(c, pid, n)) return -1;
+  Policy& P = c->pol[pid];
+  float bp[2];
+  HIPCHK(hipMemcpyAsync(m, P.m, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(v, P.v, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(bp, P.beta_pow, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (b1p) *b1p = bp[0];
+  if (b2p) *b2p = bp[1];
+  return 0;
+}
+
+int ddrl_filter_set(ddrl_ctx* c, double n, const double* M, const double* S) {
+  CHK_CTX(c);
+  const int D = c->cfg.obs_full_dim;
+  HIPCHK(hipMemcpyAsync(c->f_n, &n, 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->f_M, M, D * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->f_S, S, D * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int ddrl_filter_get(ddrl_ctx* c, double* n, double* M, double* S) {
+  CHK_CTX(c);
+  const int D = c->cfg.obs_full_dim;
+  HIPCHK(hipMemcpyAsync(n, c->f_n, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(M, c->f_M, D * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(S, c->f_S, D * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int ddrl_observe(ddrl_ctx* c, const float* obs) {
+  CHK_CTX(c);
+  if (!obs) return fail("null observation buffer");
+  const ddrl_cfg& g = c->cfg;
+  launch_filter_push(c->stream, obs, g.n_envs, g.obs_full_dim, c->f_n, c->f_M, c->f_S, c->f_normc,
+                     g.filter_update, g.filter_enabled);
+  if (g.model_kind == DDRL_MODEL_FFN)
+    launch_observe_ffn(c->stream, c->route, obs, c->f_normc, g.filter_enabled ? g.filter_clip : 0.f,
+                       c->stage_tab);
+  else
+    launch_observe_gnn(c->stream, c->route, obs, c->f_normc, g.filter_enabled ? g.filter_clip : 0.f,
+                       c->pol[0].stage);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+static ActArgs make_act(ddrl_ctx* c, int t, const float* eps, float* actions, int mode) {
+  ActArgs aa{};
+  for (int p = 0; p < c->cfg.n_policies; ++p) {
+    Policy& P = c->pol[p];
+    aa.theta[p] = P.theta; aa.stage[p] = P.stage; aa.rec[p] = P.rec; aa.last_v[p] = P.last_v;
+    aa.lay[p] = P.lay; aa.C[p] = P.C;
+  }
+  aa.t = t; aa.eps = eps; aa.actions = actions; aa.bootstrap = mode;
+  return aa;
+}
+
+static int launch_act(ddrl_ctx* c, const ActArgs& aa) {
+  if (c->cfg.model_kind == DDRL_MODEL_FFN) launch_act_ffn(c->stream, c->route, aa);
+  else launch_act_gnn(c->stream, c->route, aa);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int ddrl_act(ddrl_ctx* c, int t, const float* eps, float* actions) {
+  CHK_CTX(c);
+  if (t < 0 || t >= c->cfg.frag_len) return fail("t out of range");
+  if (!eps || !actions) return fail("null eps/actions buffer");
+  return launch_act(c, make_act(c, t, eps, actions, 0));
+}
+
+int ddrl_bootstrap(ddrl_ctx* c) {
+  CHK_CTX(c);
+  return launch_act(c, make_act(c, 0, nullptr, nullptr, 1));
+}
+
+int ddrl_reward(ddrl_ctx* c, int t, const float* fw, const float* cfrc, const float* actions,
+                const uint8_t* done) {
+  CHK_CTX(c);
+  if (t < 0 || t >= c->cfg.frag_len) return fail("t out of range");
+  if (!fw || !cfrc || !actions) return fail("null reward input");
+  const ddrl_cfg& g = c->cfg;
+  RewardArgs ra{};
+  ra.P = g.n_policies; ra.N = g.n_envs; ra.n_agents = g.n_agents; ra.mode = g.reward_mode;
+  ra.ctrl_w = g.ctrl_cost_weight; ra.contact_w = g.contact_cost_weight; ra.t = t;
+  for (int p = 0; p < g.n_policies; ++p) {
+    ra.k[p] = c->pol[p].k; ra.rec[p] = c->pol[p].rec; ra.lay[p] = c->pol[p].lay;
+    for (int s = 0; s < c->pol[p].k; ++s) {
+      ra.policy_of_agent[c->pol[p].agents[s]] = p;
+      ra.slot_of_agent[c->pol[p].agents[s]] = s;
+    }
+  }
+  for (int j = 0; j < g.n_agents; ++j) {
+    ra.n_act[j] = g.act_dim;
+    for (int a = 0; a < 8; ++a) ra.act_index[j][a] = g.act_index[j][a];
+    ra.n_contact[j] = g.n_contact[j];
+    for (int b = 0; b < 14; ++b) {
+      ra.contact_index[j][b] = g.contact_index[j][b];
+      ra.contact_weight[j][b] = g.contact_weight[j][b];
+    }
+  }
+  launch_reward(c->stream, ra, fw, cfrc, actions, done, c->done_tn);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int ddrl_step_host(ddrl_ctx* c, int t, const float* obs_h, const float* eps_h, float* act_h) {
+  CHK_CTX(c);
+  const ddrl_cfg& g = c->cfg;
+  HIPCHK(hipMemcpyAsync(c->h_obs, obs_h, (size_t)g.n_envs * g.obs_full_dim * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->h_eps, eps_h, (size_t)g.n_envs * g.n_agents * g.act_dim * 4, hipMemcpyHostToDevice,
+                        c->stream));
+  if (ddrl_observe(c, c->h_obs)) return -1;
+  if (ddrl_act(c, t, c->h_eps, c->h_act)) return -1;
+  HIPCHK(hipMemcpyAsync(act_h, c->h_act, (size_t)g.n_envs * 8 * 4, hipMemcpyDeviceToHost, c->stream));
+  return 0;
+}
+
+int ddrl_gae(ddrl_ctx* c) {
+  CHK_CTX(c);
+  const ddrl_cfg& g = c->cfg;
+  for (int p = 0; p < g.n_policies; ++p) {
+    Policy& P = c->pol[p];
+    GaeArgs ga{};
+    ga.rec = P.rec; ga.lay = P.lay; ga.C = P.C; ga.T = g.frag_len; ga.N = g.n_envs; ga.k = P.k;
+    ga.last_v = P.last_v; ga.done_tn = c->done_tn; ga.gamma = g.gamma; ga.lambda_ = g.lambda_;
+    ga.partials = P.partials; ga.adv_norm = P.adv_norm;
+    launch_gae(c->stream, ga);
+  }
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+static UpdateHyper make_hyper(ddrl_ctx* c, int P) {
+  const ddrl_cfg& g = c->cfg;
+  UpdateHyper h{};
+  h.clip = g.clip_param; h.vf_clip = g.vf_clip_param; h.vf_coeff = g.vf_loss_coeff;
+  h.ent_coeff = g.entropy_coeff; h.lr = g.lr; h.grad_clip = g.grad_clip; h.b1 = g.adam_beta1;
+  h.b2 = g.adam_beta2; h.eps = g.adam_eps; h.vf_mode = g.vf_clip_mode; h.P = P;
+  return h;
+}
+
+static UpdateArgs make_update(ddrl_ctx* c, int p, const int32_t* shuffle, const int32_t* perm, float kl) {
+  Policy& P = c->pol[p];
+  UpdateArgs u{};
+  u.rec = P.rec; u.lay = P.lay; u.d = P.d; u.A = c->cfg.act_dim; u.R = P.R;
+  u.shuffle = shuffle; u.perm = perm; u.nb = P.nb; u.n_epochs = c->cfg.num_sgd_iter;
+  u.max_steps = -1; u.step0 = 0;
+  u.theta = P.theta; u.m = P.m; u.v = P.v; u.beta_pow = P.beta_pow; u.stats = P.stats;
+  u.adv_norm = P.adv_norm; u.grad_out = nullptr; u.gscr = P.grad; u.kl_coeff = kl;
+  return u;
+}
+
+int ddrl_ppo_update(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const int32_t* const* perm,
+                    const float* kl, int max_steps) {
+  CHK_CTX(c);
+  if (!shuffle || !perm || !kl) return fail("null update argument");
+  UpdateArgs ua[DDRL_MAXP];
+  int n = 0;
+  for (int p = 0; p < c->cfg.n_policies; ++p) {
+    if (!(mask & (1 << p))) continue;
+    if (!shuffle[p] || !perm[p]) return fail("null shuffle/perm for a masked policy");
+    ua[n] = make_update(c, p, shuffle[p], perm[p], kl[p]);
+    ua[n].max_steps = max_steps;
+    const int total = c->cfg.num_sgd_iter * c->pol[p].nb;
+    c->pol[p].last_steps = max_steps >= 0 ? std::min(total, max_steps) : total;
+    ++n;
+  }
+  if (n == 0) return 0;
+  int maxd = 0;  // KS1 instance must cover the widest policy (narrower ones are zero-padded)
+  for (int i = 0; i < n; ++i) maxd = std::max(maxd, ua[i].d);
+  UpdateHyper h = make_hyper(c, n);
+  // pageable source: the runtime stages (or blocks on) the copy before returning
+  HIPCHK(hipMemcpyAsync(c->d_uargs, ua, sizeof(UpdateArgs) * n, hipMemcpyHostToDevice, c->stream));
+  if (c->cfg.model_kind == DDRL_MODEL_FFN)
+    launch_update_ffn(c->stream, c->d_uargs, h, 128, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim, maxd);
+  else
+    launch_update_gnn(c->stream, c->d_uargs, h, 128, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int ddrl_ppo_stats(ddrl_ctx* c, int pid, float* host, size_t n_steps) {
+  CHK_CTX(c);
+  if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
+  const size_t cap = (size_t)c->cfg.num_sgd_iter * c->pol[pid].nb;
+  if (n_steps > cap) return fail("more stats requested than the schedule holds");
+  HIPCHK(hipMemcpyAsync(host, c->pol[pid].stats, n_steps * 8 * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int ddrl_ppo_grad(ddrl_ctx* c, int pid, const int32_t* rows, int n_rows, float kl, float* grad) {
+  CHK_CTX(c);
+  if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
+  if (n_rows < 1 || n_rows > 128) return fail("n_rows must be in [1, 128]");
+  if (!rows || !grad) return fail("null rows/grad");
+  UpdateArgs u = make_update(c, pid, rows, c->zero_perm, kl);
+  u.nb = 1; u.n_epochs = 1; u.max_steps = 1; u.step0 = 0; u.grad_out = grad; u.stats = nullptr;
+  UpdateHyper h = make_hyper(c, 1);
+  HIPCHK(hipMemcpyAsync(c->d_uargs, &u, sizeof(UpdateArgs), hipMemcpyHostToDevice, c->stream));
+  if (c->cfg.model_kind == DDRL_MODEL_FFN)
+    launch_update_ffn(c->stream, c->d_uargs, h, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim,
+                      c->pol[pid].d);
+  else
+    launch_update_gnn(c->stream, c->d_uargs, h, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int ddrl_ppo_apply(ddrl_ctx* c, int pid, const float* grad) {
+  CHK_CTX(c);
+  if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
+  if (!grad) return fail("null grad");
+  Policy& P = c->pol[pid];
+  launch_apply_adam(c->stream, grad, P.n_params, P.theta, P.m, P.v, P.beta_pow, make_hyper(c, 1));
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int ddrl_policy_forward(ddrl_ctx* c, int pid, const float* obs, const int32_t* node, int n,
+                        float* logits, float* values) {
+  CHK_CTX(c);
+  if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
+  if (n < 1 || !obs || !logits || !values) return fail("bad forward arguments");
+  Policy& P = c->pol[pid];
+  ForwardArgs fa{};
+  fa.theta = P.theta; fa.x = obs; fa.node = node; fa.n = n; fa.d = P.d; fa.A = c->cfg.act_dim;
+  fa.logits = logits; fa.values = values;
+  if (c->cfg.model_kind == DDRL_MODEL_FFN) launch_forward_ffn(c->stream, fa);
+  else launch_forward_gnn(c->stream, fa);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int ddrl_records_get(ddrl_ctx* c, int pid, float* host, size_t n) {
+  CHK_CTX(c);
+  if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
+  const Policy& P = c->pol[pid];
+  if (n != (size_t)P.R * P.lay.stride) return fail("record buffer size mismatch");
+  HIPCHK(hipMemcpyAsync(host, P.rec, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int ddrl_records_set(ddrl_ctx* c, int pid, const float* host, size_t n) {
+  CHK_CTX(c);
+  if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
+  const Policy& P = c->pol[pid];
+  if (n != (size_t)P.R * P.lay.stride) return fail("record buffer size mismatch");
+  HIPCHK(hipMemcpyAsync(P.rec, host, n * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int ddrl_adv_norm_get(ddrl_ctx* c, int pid, float* host2) {
+  CHK_CTX(c);
+  if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
+  HIPCHK(hipMemcpyAsync(host2, c->pol[pid].adv_norm, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int ddrl_adv_norm_set(ddrl_ctx* c, int pid, float mean, float den) {
+  CHK_CTX(c);
+  if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
+  float a[2] = {mean, den};
+  HIPCHK(hipMemcpyAsync(c->pol[pid].adv_norm, a, 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int ddrl_last_values_get(ddrl_ctx* c, int pid, float* host, size_t n) {
+  CHK_CTX(c);
+  if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
+  if (n != (size_t)c->pol[pid].C) return fail("last value count mismatch");
+  HIPCHK(hipMemcpyAsync(host, c->pol[pid].last_v, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int ddrl_done_set(ddrl_ctx* c, const uint8_t* host, size_t n) {
+  CHK_CTX(c);
+  if (n != (size_t)c->cfg.frag_len * c->cfg.n_envs) return fail("done buffer size mismatch");
+  HIPCHK(hipMemcpyAsync(c->done_tn, host, n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int ddrl_device_buffers(ddrl_ctx* c, int pid, void** records, void** last_v, void** params, void** adv_norm) {
+  CHK_CTX(c);
+  if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
+  Policy& P = c->pol[pid];
+  if (records) *records = P.rec;
+  if (last_v) *last_v = P.last_v;
+  if (params) *params = P.theta;
+  if (adv_norm) *adv_norm = P.adv_norm;
+  return 0;
+}
+
+}  // extern "C"

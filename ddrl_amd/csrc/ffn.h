@@ -1,0 +1,77 @@
+// FFN (fcnet, models/fcnet_glorot_uniform_init.py:17-125) parameter packing and the
+// LDS weight image shared by the rollout forward and the PPO update kernels.
+// Parameter order is the Keras / checkpoint variable order:
+//   fc_1/kernel [d,64], fc_1/bias, fc_value_1/kernel [d,64], fc_value_1/bias,
+//   fc_2/kernel [64,64], fc_2/bias, fc_value_2/kernel, fc_value_2/bias,
+//   fc_out/kernel [64,2A], fc_out/bias, value_out/kernel [64,1], value_out/bias.
+#pragma once
+#include "common.h"
+
+struct FfnOffsets {
+  int w1, b1, vw1, vb1, w2, b2, vw2, vb2, wo, bo, vo, vbo, n;
+};
+__host__ __device__ inline FfnOffsets ffn_offsets(int d, int A) {
+  FfnOffsets o;
+  o.w1 = 0;            o.b1 = d * 64;        o.vw1 = o.b1 + 64;  o.vb1 = o.vw1 + d * 64;
+  o.w2 = o.vb1 + 64;   o.b2 = o.w2 + 4096;   o.vw2 = o.b2 + 64;  o.vb2 = o.vw2 + 4096;
+  o.wo = o.vb2 + 64;   o.bo = o.wo + 64 * 2 * A;
+  o.vo = o.bo + 2 * A; o.vbo = o.vo + 64;    o.n = o.vbo + 1;
+  return o;
+}
+
+// LDS image of both branches: [pol w1 48x64][pol w2][val w1][val w2][b1 b2 vb1 vb2][wo][bo][vo][vbo]
+#define LDS_W1 (48 * 64)
+#define LDS_W2 (64 * 64)
+__device__ inline void stage_weights(const float* __restrict__ th, int d, int A, float* lds,
+                                     NetLds& P, NetLds& V, int nthreads) {
+  const FfnOffsets o = ffn_offsets(d, A);
+  const int O = 2 * A;
+  P.w1 = lds;                 P.w2 = P.w1 + LDS_W1;
+  V.w1 = P.w2 + LDS_W2;       V.w2 = V.w1 + LDS_W1;
+  P.b1 = V.w2 + LDS_W2;       P.b2 = P.b1 + 64;  V.b1 = P.b2 + 64;  V.b2 = V.b1 + 64;
+  P.wo = V.b2 + 64;           P.bo = P.wo + 64 * O;
+  V.wo = P.bo + O;            V.bo = V.wo + 64;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 48 * 64; i += nthreads) {
+    const int f = i >> 6, col = i & 63;
+    P.w1[sidx(f, col)] = f < d ? th[o.w1 + i] : 0.f;
+    V.w1[sidx(f, col)] = f < d ? th[o.vw1 + i] : 0.f;
+  }
+  for (int i = tid; i < 64 * 64; i += nthreads) {
+    const int f = i >> 6, col = i & 63;
+    P.w2[sidx(f, col)] = th[o.w2 + i];
+    V.w2[sidx(f, col)] = th[o.vw2 + i];
+  }
+  for (int i = tid; i < 64; i += nthreads) {
+    P.b1[i] = th[o.b1 + i]; P.b2[i] = th[o.b2 + i];
+    V.b1[i] = th[o.vb1 + i]; V.b2[i] = th[o.vb2 + i];
+    V.wo[i] = th[o.vo + i];
+  }
+  for (int i = tid; i < 64 * O; i += nthreads) P.wo[i] = th[o.wo + i];
+  for (int i = tid; i < O; i += nthreads) P.bo[i] = th[o.bo + i];
+  if (tid == 0) V.bo[0] = th[o.vbo];
+}
+#define LDS_WEIGHTS_FLOATS(O) (2 * LDS_W1 + 2 * LDS_W2 + 4 * 64 + 64 * (O) + (O) + 64 + 1)
+
+
+// Compile-time (A, ceil(d/4)) instantiation for the observation widths of the reference's
+// envs: d = 19/20 (FullyDecentral, Shared), 27/28 (SingleNeighbor/Diagonal/ToFront,
+// TwoSides/TwoDiags), 35/36 (Local), 43/44 (Centralized).  Any other d <= 48 runs the
+// KS1 = 12 instance (zero-padded features).
+#define DDRL_DISPATCH_A_KS1(A_, d_, FN, ...)                                   \
+  do {                                                                         \
+    const int ks1_ = ((d_) + 3) >> 2;                                          \
+    if ((A_) == 2) {                                                           \
+      if (ks1_ == 5) FN<2, 5>(__VA_ARGS__);                                    \
+      else if (ks1_ == 7) FN<2, 7>(__VA_ARGS__);                               \
+      else if (ks1_ == 9) FN<2, 9>(__VA_ARGS__);                               \
+      else if (ks1_ == 11) FN<2, 11>(__VA_ARGS__);                             \
+      else FN<2, 12>(__VA_ARGS__);                                             \
+    } else if ((A_) == 4) {                                                    \
+      if (ks1_ == 7) FN<4, 7>(__VA_ARGS__);                                    \
+      else FN<4, 12>(__VA_ARGS__);                                             \
+    } else {                                                                   \
+      if (ks1_ == 11) FN<8, 11>(__VA_ARGS__);                                  \
+      else FN<8, 12>(__VA_ARGS__);                                             \
+    }                                                                          \
+  } while (0)

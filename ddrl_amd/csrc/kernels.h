@@ -1,0 +1,118 @@
+// Host-side launch wrappers shared between the kernel translation units and the C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DDRL_MAXP 4       // policies per context
+#define DDRL_MAXAG 4      // agents per env
+#define DDRL_MAXD 48      // per-agent observation width
+#define DDRL_MAXFULL 48   // full observation width (43 / 44)
+
+// Record (one training row) layout, in floats.  Rows are time-major:
+//   row = t * C + c,  c = env * k + slot  (k agents of this policy per env).
+struct RecLayout {
+  int stride;      // floats per row (multiple of 4)
+  int obs, act, logit, logp, vf, adv, vt, rew;
+};
+
+// Per-policy routing tables for the observe / act / reward kernels.
+struct PolicyRoute {
+  int k;                    // agents of this policy per env
+  int d;                    // obs width per row (GNN: 19 features per node)
+  int agent[DDRL_MAXAG];    // agent id of each slot
+  int obs_index[DDRL_MAXAG][DDRL_MAXD];
+  int act_index[DDRL_MAXAG][8];
+};
+
+struct RouteArgs {
+  int P, N, A, full_dim, n_agents, model;   // model: 0 ffn, 1 gnn
+  PolicyRoute pol[DDRL_MAXP];
+  float leg_angle[4];
+};
+
+// ---- filter / observe (rollout.hip) ----
+void launch_filter_push(hipStream_t s, const float* obs, int N, int D, double* n_run, double* M,
+                        double* S, double* normc, int update, int enabled);
+void launch_observe_ffn(hipStream_t s, const RouteArgs& ra, const float* obs, const double* normc,
+                        float clip, float* const* stage);
+void launch_observe_gnn(hipStream_t s, const RouteArgs& ra, const float* obs, const double* normc,
+                        float clip, float* stage_x /*[N][4][23]*/);
+
+// ---- act (rollout forward + sample) ----
+struct ActArgs {
+  const float* theta[DDRL_MAXP];
+  const float* stage[DDRL_MAXP];   // [C][d] (ffn) or [N][4][23] (gnn)
+  float* rec[DDRL_MAXP];           // base of the record buffer of this policy
+  float* last_v[DDRL_MAXP];
+  RecLayout lay[DDRL_MAXP];
+  int C[DDRL_MAXP];
+  int t;                           // time index (record row block)
+  const float* eps;                // [N][n_agents][A]
+  float* actions;                  // [N][8]
+  int bootstrap;                   // 1: only value -> last_v
+};
+void launch_act_ffn(hipStream_t s, const RouteArgs& ra, const ActArgs& aa);
+void launch_act_gnn(hipStream_t s, const RouteArgs& ra, const ActArgs& aa);
+
+// ---- reward (a8) ----
+struct RewardArgs {
+  int P, N, n_agents, mode;         // mode: 0 per-leg, 1 global, 2 norm_reward
+  float ctrl_w, contact_w;
+  int policy_of_agent[DDRL_MAXAG];
+  int slot_of_agent[DDRL_MAXAG];
+  int k[DDRL_MAXP];
+  int act_index[DDRL_MAXAG][8];
+  int n_act[DDRL_MAXAG];
+  int n_contact[DDRL_MAXAG];
+  int contact_index[DDRL_MAXAG][14];
+  float contact_weight[DDRL_MAXAG][14];
+  float* rec[DDRL_MAXP];
+  RecLayout lay[DDRL_MAXP];
+  int t;
+};
+void launch_reward(hipStream_t s, const RewardArgs& ra, const float* fw, const float* cfrc,
+                   const float* actions, const uint8_t* done, uint8_t* done_tn);
+
+// ---- GAE + standardization statistics ----
+struct GaeArgs {
+  float* rec; RecLayout lay; int C, T, N, k;
+  const float* last_v; const uint8_t* done_tn;
+  double gamma, lambda_;
+  double* partials;   // [nblocks][2]
+  float* adv_norm;    // [2]: mean, max(1e-4, std)
+};
+void launch_gae(hipStream_t s, const GaeArgs& g);
+
+// ---- PPO update (fused persistent minibatch loop) ----
+struct UpdateArgs {
+  const float* rec; RecLayout lay;
+  int d, A, R;                 // obs width, action dim, rows of this policy
+  const int32_t* shuffle;      // [R]
+  const int32_t* perm;         // [E][nb]
+  int nb, n_epochs, max_steps, step0;
+  float* theta; float* m; float* v; float* beta_pow;   // beta_pow[2]
+  float* stats;                // [steps][8]
+  const float* adv_norm;       // [2]
+  float* grad_out;             // optional: write raw (unclipped) grads and stop (DDP)
+  float* gscr;                 // [n_params] gradient scratch (L2 resident)
+  float kl_coeff;
+};
+struct UpdateHyper {
+  float clip, vf_clip, vf_coeff, ent_coeff, lr, grad_clip, b1, b2, eps;
+  int vf_mode;
+  int P;
+};
+// ua_dev: device array of h.P UpdateArgs (one persistent workgroup per entry)
+void launch_update_ffn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHyper& h, int nrows, float inv_n, int A, int d);
+void launch_update_gnn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHyper& h, int nrows, float inv_n, int A);
+// clip_by_global_norm + tf1 Adam on a flat (all-reduced) gradient vector
+void launch_apply_adam(hipStream_t s, const float* grad, int n, float* theta, float* m, float* v,
+                       float* beta_pow, const UpdateHyper& h);
+
+// ---- ModelV2.forward / value_function on arbitrary rows ----
+struct ForwardArgs {
+  const float* theta; const float* x; const int32_t* node; int n, d, A;
+  float* logits; float* values;
+};
+void launch_forward_ffn(hipStream_t s, const ForwardArgs& fa);
+void launch_forward_gnn(hipStream_t s, const ForwardArgs& fa);

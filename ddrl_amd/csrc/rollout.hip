@@ -1,0 +1,316 @@
+// Rollout-side kernels: env-side MeanStdFilter (a2), observation routing (a1/a3),
+// fused per-policy forward + DiagGaussian sampling + action scatter (a4/a6/a7),
+// per-leg rewards (a8).
+//
+// Reference: simulation_envs/quantruped_adaptor_multi_environment.py:83-85 (normalize),
+// :124-136 (distribute_observations), :160-212 (contact cost, rewards, concatenate_actions);
+// models/fcnet_glorot_uniform_init.py:120-125 (forward / value_function);
+// RLlib DiagGaussian sampling with clip_actions=True.
+#include "common.h"
+#include "kernels.h"
+#include "ffn.h"
+
+// ------------------------------------------------------------------------------------
+// a2: batched MeanStdFilter push.  One workgroup per observation column.  The batch's
+// (n, mean, M2) is reduced in fp64 with a fixed order and merged into the running stat
+// with RunningStat.update (Chan's parallel formula); normalization constants
+// (mean, std + 1e-8) for the whole batch are written afterwards -- a batched
+// MeanStdFilter call pushes every row before normalizing.
+// ------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_filter_push(const float* __restrict__ obs, int N, int D,
+                                                     double* n_run, double* M, double* S,
+                                                     double* normc, int update, int enabled) {
+  const int j = blockIdx.x;
+  __shared__ double red[4];
+  __shared__ double sh_mean;
+  const int tid = threadIdx.x, w = tid >> 6;
+  double mean_b = 0.0, s_b = 0.0;
+  if (enabled && update) {
+    double acc = 0.0;
+    for (int e = tid; e < N; e += 256) acc += (double)obs[(size_t)e * D + j];
+    acc = wave_sum_d(acc);
+    if ((tid & 63) == 0) red[w] = acc;
+    __syncthreads();
+    if (tid == 0) sh_mean = ((red[0] + red[1]) + (red[2] + red[3])) / (double)N;
+    __syncthreads();
+    mean_b = sh_mean;
+    double acc2 = 0.0;
+    for (int e = tid; e < N; e += 256) {
+      double dlt = (double)obs[(size_t)e * D + j] - mean_b;
+      acc2 += dlt * dlt;
+    }
+    acc2 = wave_sum_d(acc2);
+    __syncthreads();
+    if ((tid & 63) == 0) red[w] = acc2;
+    __syncthreads();
+    s_b = (red[0] + red[1]) + (red[2] + red[3]);
+  }
+  if (tid == 0) {
+    double n1 = n_run[0];
+    double Mj = M[j], Sj = S[j];
+    if (enabled && update) {
+      const double n2 = (double)N, n = n1 + n2;
+      const double delta = Mj - mean_b;
+      Mj = (n1 * Mj + n2 * mean_b) / n;
+      Sj = Sj + s_b + delta * delta * n1 * n2 / n;
+      n1 = n;
+      M[j] = Mj;
+      S[j] = Sj;
+    }
+    const double var = n1 > 1.0 ? Sj / (n1 - 1.0) : Mj * Mj;
+    normc[2 * j] = enabled ? Mj : 0.0;
+    normc[2 * j + 1] = enabled ? sqrt(var) + 1e-8 : 1.0;
+  }
+}
+
+__global__ void k_filter_count(double* n_run, int N) { n_run[0] += (double)N; }
+
+void launch_filter_push(hipStream_t s, const float* obs, int N, int D, double* n_run, double* M,
+                        double* S, double* normc, int update, int enabled) {
+  hipLaunchKernelGGL(k_filter_push, dim3(D), dim3(256), 0, s, obs, N, D, n_run, M, S, normc,
+                     update, enabled);
+  if (enabled && update) hipLaunchKernelGGL(k_filter_count, dim3(1), dim3(1), 0, s, n_run, N);
+}
+
+__device__ __forceinline__ float norm_obs(float x, const double* normc, int idx, float clip) {
+  double z = ((double)x - normc[2 * idx]) / normc[2 * idx + 1];
+  if (clip > 0.f) z = fmin(fmax(z, -(double)clip), (double)clip);
+  return (float)z;
+}
+
+// a1: per-agent gather of the normalized observation into stage[p][c][f].
+__global__ void k_observe_ffn(RouteArgs ra, const float* __restrict__ obs,
+                              const double* __restrict__ normc, float clip, float* const* stage_tab) {
+  const int p = blockIdx.y;
+  const PolicyRoute& pr = ra.pol[p];
+  const int C = ra.N * pr.k;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= C * pr.d) return;
+  const int c = gid / pr.d, f = gid - c * pr.d;
+  const int e = c / pr.k, slot = c - e * pr.k;
+  const int idx = pr.obs_index[slot][f];
+  stage_tab[p][(size_t)c * pr.d + f] = norm_obs(obs[(size_t)e * ra.full_dim + idx], normc, idx, clip);
+}
+
+void launch_observe_ffn(hipStream_t s, const RouteArgs& ra, const float* obs, const double* normc,
+                        float clip, float* const* stage) {
+  int maxw = 0;
+  for (int p = 0; p < ra.P; ++p) maxw = max(maxw, ra.N * ra.pol[p].k * ra.pol[p].d);
+  dim3 grid((maxw + 255) / 256, ra.P);
+  hipLaunchKernelGGL(k_observe_ffn, grid, dim3(256), 0, s, ra, obs, normc, clip, stage);
+}
+
+// a3: graph observation X[env][node] = [normalized 19 features | ego quaternion (raw obs)].
+__global__ void k_observe_gnn(RouteArgs ra, const float* __restrict__ obs,
+                              const double* __restrict__ normc, float clip, float* __restrict__ X) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= ra.N * 4) return;
+  const int e = gid >> 2, n = gid & 3;
+  const PolicyRoute& pr = ra.pol[0];
+  const float* o = obs + (size_t)e * ra.full_dim;
+  float* x = X + (size_t)gid * 23;
+  for (int f = 0; f < 19; ++f) {
+    const int idx = pr.obs_index[n][f];
+    x[f] = norm_obs(o[idx], normc, idx, clip);
+  }
+  // leg_encoding_ego: quat_mul(obs[1:5], [0, 0, sin(a/2), cos(a/2)]) in fp64
+  const double rad = (double)ra.leg_angle[n] / 2.0 * (3.14159265358979323846 / 180.0);
+  const double z2 = sin(rad), w2 = cos(rad);
+  const double x1 = o[1], y1 = o[2], z1 = o[3], w1 = o[4];
+  x[19] = (float)(x1 * w2 + y1 * z2 - z1 * 0.0 + w1 * 0.0);
+  x[20] = (float)(-x1 * z2 + y1 * w2 + z1 * 0.0 + w1 * 0.0);
+  x[21] = (float)(x1 * 0.0 - y1 * 0.0 + z1 * w2 + w1 * z2);
+  x[22] = (float)(-x1 * 0.0 - y1 * 0.0 - z1 * z2 + w1 * w2);
+}
+
+void launch_observe_gnn(hipStream_t s, const RouteArgs& ra, const float* obs, const double* normc,
+                        float clip, float* stage_x) {
+  hipLaunchKernelGGL(k_observe_gnn, dim3((ra.N * 4 + 255) / 256), dim3(256), 0, s, ra, obs, normc,
+                     clip, stage_x);
+}
+
+// ------------------------------------------------------------------------------------
+// a4 + a6 + a7: fused rollout forward.  Workgroup = 4 waves = 64 rows of ONE policy
+// (grid.y = policy).  The policy's weights are staged once into LDS in the swizzled
+// image; each wave runs both branches for its 16 rows from registers (MFMA 16x16x4 f32),
+// samples a = mean + exp(log_std) * eps, computes logp, writes the training record and
+// scatters clip(a, -1, 1) into the env action vector.
+// ------------------------------------------------------------------------------------
+template <int A, int KS1>
+__global__ void __launch_bounds__(256) k_act_ffn(RouteArgs ra, ActArgs aa) {
+  constexpr int O = 2 * A;
+  extern __shared__ float lds[];
+  const int p = blockIdx.y;
+  const PolicyRoute& pr = ra.pol[p];
+  const int C = aa.C[p];
+  const int row0 = blockIdx.x * 64;
+  if (row0 >= C) return;
+  const int d = pr.d;
+  NetLds PW, VW;
+  stage_weights(aa.theta[p], d, A, lds, PW, VW, 256);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4, w = threadIdx.x >> 6;
+  const int row = row0 + 16 * w + c;
+  const bool valid = row < C;
+  const float* xs = aa.stage[p] + (size_t)(valid ? row : 0) * d;
+  float xop[12];
+#pragma unroll
+  for (int s = 0; s < 12; ++s) {
+    const int f = 4 * s + q;
+    xop[s] = (s < KS1 && f < d && valid) ? xs[f] : 0.f;
+  }
+  floatx4 h1[4], h2[4];
+  float vout[1];
+  ffn_branch_fwd<1, KS1>(VW, xop, h1, h2, vout);
+  const RecLayout& L = aa.lay[p];
+  if (aa.bootstrap) {
+    if (valid && q == 0) aa.last_v[p][row] = vout[0];
+    return;
+  }
+  float logits[O];
+  ffn_branch_fwd<O, KS1>(PW, xop, h1, h2, logits);
+  if (!valid) return;
+  float* rp = aa.rec[p] + ((size_t)aa.t * C + row) * L.stride;
+  const int e = row / pr.k, slot = row - e * pr.k;
+  const int agent = pr.agent[slot];
+  // sample + logp (DiagGaussian, RLlib 1.0): a = mean + std * eps
+  float logp = -0.5f * (float)(DDRL_LOG2PI * A);
+  float act[A];
+#pragma unroll
+  for (int j = 0; j < A; ++j) {
+    const float mu = logits[j], ls = logits[A + j];
+    const float sd = expf(ls);
+    const float eps = aa.eps[((size_t)e * ra.n_agents + agent) * A + j];
+    act[j] = mu + sd * eps;
+    const float z = (act[j] - mu) / sd;
+    logp -= 0.5f * z * z;
+    logp -= ls;
+  }
+  // q-lanes split the record stores
+  for (int f = q; f < d; f += 4) rp[L.obs + f] = xs[f];
+  if (q == 0) {
+#pragma unroll
+    for (int j = 0; j < A; ++j) {
+      rp[L.act + j] = act[j];
+      aa.actions[(size_t)e * 8 + pr.act_index[slot][j]] = fminf(fmaxf(act[j], -1.f), 1.f);
+    }
+  } else if (q == 1) {
+#pragma unroll
+    for (int j = 0; j < O; ++j) rp[L.logit + j] = logits[j];
+  } else if (q == 2) {
+    rp[L.logp] = logp;
+    rp[L.vf] = vout[0];
+  }
+}
+
+template <int A, int KS1>
+static void launch_act_t(hipStream_t s, dim3 grid, const RouteArgs& ra, const ActArgs& aa) {
+  hipLaunchKernelGGL((k_act_ffn<A, KS1>), grid, dim3(256), LDS_WEIGHTS_FLOATS(2 * A) * 4, s, ra, aa);
+}
+
+void launch_act_ffn(hipStream_t s, const RouteArgs& ra, const ActArgs& aa) {
+  int maxC = 0;
+  for (int p = 0; p < ra.P; ++p) maxC = max(maxC, aa.C[p]);
+  dim3 grid((maxC + 63) / 64, ra.P);
+  int maxd = 0;
+  for (int p = 0; p < ra.P; ++p) maxd = max(maxd, ra.pol[p].d);
+  DDRL_DISPATCH_A_KS1(ra.A, maxd, launch_act_t, s, grid, ra, aa);
+}
+
+// ------------------------------------------------------------------------------------
+// a8: per-leg (or global / normalized) reward of each agent; fp64 like the reference.
+// ------------------------------------------------------------------------------------
+__global__ void k_reward(RewardArgs ra, const float* __restrict__ fw, const float* __restrict__ cfrc,
+                         const float* __restrict__ actions, const uint8_t* __restrict__ done,
+                         uint8_t* __restrict__ done_tn) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= ra.N) return;
+  const float* cf = cfrc + (size_t)e * 14 * 6;
+  const float* a8 = actions + (size_t)e * 8;
+  const double fwd = fw[e];
+  const int na = ra.n_agents;
+  double ctrl_all = 0.0, contact_all = 0.0;
+  if (ra.mode == 1) {
+    for (int i = 0; i < 8; ++i) ctrl_all += (double)a8[i] * a8[i];
+    for (int i = 0; i < 14 * 6; ++i) {
+      const double v = fmin(fmax((double)cf[i], -1.0), 1.0);
+      contact_all += v * v;
+    }
+    contact_all *= ra.contact_w;
+  }
+  for (int j = 0; j < na; ++j) {
+    double r;
+    if (ra.mode == 1) {
+      r = (fwd - ra.ctrl_w * ctrl_all - contact_all) / na;
+    } else {
+      double ctrl = 0.0;
+      for (int i = 0; i < ra.n_act[j]; ++i) {
+        const double a = a8[ra.act_index[j][i]];
+        ctrl += a * a;
+      }
+      double contact = 0.0;
+      for (int b = 0; b < ra.n_contact[j]; ++b) {
+        const float* body = cf + ra.contact_index[j][b] * 6;
+        double sb = 0.0;
+        for (int k = 0; k < 6; ++k) {
+          const double v = fmin(fmax((double)body[k], -1.0), 1.0);
+          sb += ra.contact_w * v * v * ra.contact_weight[j][b];
+        }
+        contact += sb;
+      }
+      r = ra.mode == 2 ? fwd - na * (ra.ctrl_w * ctrl + contact)
+                       : fwd / na - ra.ctrl_w * ctrl - contact;
+    }
+    const int p = ra.policy_of_agent[j], slot = ra.slot_of_agent[j];
+    const size_t C = (size_t)ra.N * ra.k[p];
+    float* rp = ra.rec[p] + ((size_t)ra.t * C + (size_t)e * ra.k[p] + slot) * ra.lay[p].stride;
+    rp[ra.lay[p].rew] = (float)r;
+  }
+  done_tn[(size_t)ra.t * ra.N + e] = done ? done[e] : 0;
+}
+
+void launch_reward(hipStream_t s, const RewardArgs& ra, const float* fw, const float* cfrc,
+                   const float* actions, const uint8_t* done, uint8_t* done_tn) {
+  hipLaunchKernelGGL(k_reward, dim3((ra.N + 255) / 256), dim3(256), 0, s, ra, fw, cfrc, actions,
+                     done, done_tn);
+}
+
+// ------------------------------------------------------------------------------------
+// ModelV2.forward + value_function (fcnet_glorot_uniform_init.py:120-125) on n rows.
+// ------------------------------------------------------------------------------------
+template <int A, int KS1>
+__global__ void __launch_bounds__(256) k_forward_ffn(ForwardArgs fa) {
+  constexpr int O = 2 * A;
+  extern __shared__ float lds[];
+  NetLds PW, VW;
+  stage_weights(fa.theta, fa.d, A, lds, PW, VW, 256);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4, w = threadIdx.x >> 6;
+  const int row = blockIdx.x * 64 + 16 * w + c;
+  const bool valid = row < fa.n;
+  const int d = fa.d;
+  float xop[12];
+#pragma unroll
+  for (int s = 0; s < 12; ++s) {
+    const int f = 4 * s + q;
+    xop[s] = (valid && s < KS1 && f < d) ? fa.x[(size_t)row * d + f] : 0.f;
+  }
+  floatx4 h1[4], h2[4];
+  float vout[1], logits[O];
+  ffn_branch_fwd<1, KS1>(VW, xop, h1, h2, vout);
+  ffn_branch_fwd<O, KS1>(PW, xop, h1, h2, logits);
+  if (!valid) return;
+  if (q == 0) fa.values[row] = vout[0];
+  for (int j = q; j < O; j += 4) fa.logits[(size_t)row * O + j] = logits[j];
+}
+
+template <int A, int KS1>
+static void launch_forward_t(hipStream_t s, dim3 grid, const ForwardArgs& fa) {
+  hipLaunchKernelGGL((k_forward_ffn<A, KS1>), grid, dim3(256), LDS_WEIGHTS_FLOATS(2 * A) * 4, s, fa);
+}
+
+void launch_forward_ffn(hipStream_t s, const ForwardArgs& fa) {
+  dim3 grid((fa.n + 63) / 64);
+  DDRL_DISPATCH_A_KS1(fa.A, fa.d, launch_forward_t, s, grid, fa);
+}

@@ -1,0 +1,270 @@
+"""ctypes binding of libddrl_hip.so (include/ddrl_hip.h).
+
+The HIP library is the only compute path: if it is missing or fails to load, every entry
+point raises.  There is no CPU fallback.  Device buffers are passed as raw pointers (for
+example torch tensors' data_ptr()); torch is plumbing for memory and streams only.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libddrl_hip.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "ddrl_hip.h")
+
+MAX_P, MAX_AG, MAX_OBS = 4, 4, 48
+MODEL_FFN, MODEL_GNN = 0, 1
+REWARD_PER_LEG, REWARD_GLOBAL, REWARD_NORM = 0, 1, 2
+VF_CLIP_RAY10, VF_CLIP_SQUARED = 0, 1
+
+i32, f32 = C.c_int32, C.c_float
+
+
+class DdrlCfg(C.Structure):
+    _fields_ = [
+        ("n_envs", i32), ("frag_len", i32), ("obs_full_dim", i32), ("n_agents", i32),
+        ("n_policies", i32), ("model_kind", i32), ("act_dim", i32),
+        ("agent_policy", i32 * MAX_AG), ("obs_dim", i32 * MAX_P),
+        ("obs_index", (i32 * MAX_OBS) * MAX_AG), ("act_index", (i32 * 8) * MAX_AG),
+        ("n_contact", i32 * MAX_AG), ("contact_index", (i32 * 14) * MAX_AG),
+        ("contact_weight", (f32 * 14) * MAX_AG), ("leg_angle_deg", f32 * MAX_AG),
+        ("filter_enabled", i32), ("filter_update", i32), ("filter_clip", f32),
+        ("reward_mode", i32), ("ctrl_cost_weight", f32), ("contact_cost_weight", f32),
+        ("gamma", f32), ("lambda_", f32), ("clip_param", f32), ("vf_clip_param", f32),
+        ("vf_loss_coeff", f32), ("entropy_coeff", f32), ("lr", f32), ("grad_clip", f32),
+        ("adam_beta1", f32), ("adam_beta2", f32), ("adam_eps", f32),
+        ("vf_clip_mode", i32), ("sgd_minibatch_size", i32), ("num_sgd_iter", i32),
+    ]
+
+
+VP = C.c_void_p
+_SIGS = {
+    "ddrl_abi_version": ([], C.c_int),
+    "ddrl_last_error": ([], C.c_char_p),
+    "ddrl_ctx_create": ([C.POINTER(DdrlCfg), C.c_int, C.POINTER(VP)], C.c_int),
+    "ddrl_ctx_destroy": ([VP], C.c_int),
+    "ddrl_set_stream": ([VP, VP], C.c_int),
+    "ddrl_synchronize": ([VP], C.c_int),
+    "ddrl_param_count": ([VP, C.c_int, C.POINTER(C.c_int64)], C.c_int),
+    "ddrl_record_layout": ([VP, C.c_int, C.POINTER(i32)], C.c_int),
+    "ddrl_params_set": ([VP, C.c_int, VP, C.c_size_t], C.c_int),
+    "ddrl_params_get": ([VP, C.c_int, VP, C.c_size_t], C.c_int),
+    "ddrl_adam_set": ([VP, C.c_int, VP, VP, C.c_size_t, f32, f32], C.c_int),
+    "ddrl_adam_get": ([VP, C.c_int, VP, VP, C.c_size_t, C.POINTER(f32), C.POINTER(f32)], C.c_int),
+    "ddrl_filter_set": ([VP, C.c_double, VP, VP], C.c_int),
+    "ddrl_filter_get": ([VP, C.POINTER(C.c_double), VP, VP], C.c_int),
+    "ddrl_observe": ([VP, VP], C.c_int),
+    "ddrl_act": ([VP, C.c_int, VP, VP], C.c_int),
+    "ddrl_reward": ([VP, C.c_int, VP, VP, VP, VP], C.c_int),
+    "ddrl_bootstrap": ([VP], C.c_int),
+    "ddrl_step_host": ([VP, C.c_int, VP, VP, VP], C.c_int),
+    "ddrl_gae": ([VP], C.c_int),
+    "ddrl_ppo_update": ([VP, C.c_int, C.POINTER(VP), C.POINTER(VP), C.POINTER(f32), C.c_int], C.c_int),
+    "ddrl_ppo_stats": ([VP, C.c_int, VP, C.c_size_t], C.c_int),
+    "ddrl_ppo_grad": ([VP, C.c_int, VP, C.c_int, f32, VP], C.c_int),
+    "ddrl_ppo_apply": ([VP, C.c_int, VP], C.c_int),
+    "ddrl_policy_forward": ([VP, C.c_int, VP, VP, C.c_int, VP, VP], C.c_int),
+    "ddrl_device_buffers": ([VP, C.c_int, C.POINTER(VP), C.POINTER(VP), C.POINTER(VP), C.POINTER(VP)], C.c_int),
+    "ddrl_records_get": ([VP, C.c_int, VP, C.c_size_t], C.c_int),
+    "ddrl_records_set": ([VP, C.c_int, VP, C.c_size_t], C.c_int),
+    "ddrl_adv_norm_get": ([VP, C.c_int, VP], C.c_int),
+    "ddrl_adv_norm_set": ([VP, C.c_int, f32, f32], C.c_int),
+    "ddrl_last_values_get": ([VP, C.c_int, VP, C.c_size_t], C.c_int),
+    "ddrl_done_set": ([VP, VP, C.c_size_t], C.c_int),
+}
+
+_lib = None
+
+
+class DdrlError(RuntimeError):
+    pass
+
+
+def header_symbols(path=HEADER):
+    """Function names declared in include/ddrl_hip.h."""
+    txt = open(path).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(ddrl_\w+)\s*\(", txt, re.M)))
+
+
+def load(path: str = LIB_PATH):
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise DdrlError(f"{path} is missing: build it with `python -m ddrl_amd.build` "
+                        "(the HIP library is the only compute path; there is no fallback)")
+    lib = C.CDLL(path)
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = lib
+    return lib
+
+
+def _ck(rc):
+    if rc != 0:
+        raise DdrlError(load().ddrl_last_error().decode())
+
+
+def _ptr(x):
+    """Device/host pointer of a torch tensor, numpy array, int or None."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if isinstance(x, np.ndarray):
+        assert x.flags["C_CONTIGUOUS"]
+        return x.ctypes.data
+    if hasattr(x, "data_ptr"):
+        assert x.is_contiguous()
+        return x.data_ptr()
+    raise TypeError(type(x))
+
+
+class Context:
+    """One device + stream + rollout shard (a ddrl_ctx)."""
+
+    def __init__(self, cfg: DdrlCfg, device: int = 0, stream: int | None = None):
+        self.lib = load()
+        self.cfg = cfg
+        h = VP()
+        _ck(self.lib.ddrl_ctx_create(C.byref(cfg), device, C.byref(h)))
+        self.h = h
+        self.device = device
+        if stream is not None:
+            self.set_stream(stream)
+        self.n_params = []
+        self.layout = []
+        for p in range(cfg.n_policies):
+            n = C.c_int64()
+            _ck(self.lib.ddrl_param_count(h, p, C.byref(n)))
+            self.n_params.append(int(n.value))
+            lay = (i32 * 10)()
+            _ck(self.lib.ddrl_record_layout(h, p, lay))
+            self.layout.append(dict(zip(
+                ["stride", "obs", "act", "logit", "logp", "vf", "adv", "vt", "rew", "C"], list(lay))))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.ddrl_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_stream(self, stream: int):
+        _ck(self.lib.ddrl_set_stream(self.h, stream))
+
+    def synchronize(self):
+        _ck(self.lib.ddrl_synchronize(self.h))
+
+    # ---- state ----
+    def params_set(self, pid, flat):
+        a = np.ascontiguousarray(flat, np.float32)
+        _ck(self.lib.ddrl_params_set(self.h, pid, a.ctypes.data, a.size))
+
+    def params_get(self, pid):
+        a = np.empty(self.n_params[pid], np.float32)
+        _ck(self.lib.ddrl_params_get(self.h, pid, a.ctypes.data, a.size))
+        return a
+
+    def adam_set(self, pid, m, v, b1p, b2p):
+        m = np.ascontiguousarray(m, np.float32)
+        v = np.ascontiguousarray(v, np.float32)
+        _ck(self.lib.ddrl_adam_set(self.h, pid, m.ctypes.data, v.ctypes.data, m.size, b1p, b2p))
+
+    def adam_get(self, pid):
+        n = self.n_params[pid]
+        m, v = np.empty(n, np.float32), np.empty(n, np.float32)
+        b1, b2 = f32(), f32()
+        _ck(self.lib.ddrl_adam_get(self.h, pid, m.ctypes.data, v.ctypes.data, n, C.byref(b1), C.byref(b2)))
+        return m, v, b1.value, b2.value
+
+    def filter_set(self, n, M, S):
+        M = np.ascontiguousarray(M, np.float64)
+        S = np.ascontiguousarray(S, np.float64)
+        _ck(self.lib.ddrl_filter_set(self.h, float(n), M.ctypes.data, S.ctypes.data))
+
+    def filter_get(self):
+        D = self.cfg.obs_full_dim
+        n = C.c_double()
+        M, S = np.empty(D), np.empty(D)
+        _ck(self.lib.ddrl_filter_get(self.h, C.byref(n), M.ctypes.data, S.ctypes.data))
+        return n.value, M, S
+
+    def records_get(self, pid):
+        lay = self.layout[pid]
+        a = np.empty((self.cfg.frag_len * lay["C"], lay["stride"]), np.float32)
+        _ck(self.lib.ddrl_records_get(self.h, pid, a.ctypes.data, a.size))
+        return a
+
+    def records_set(self, pid, rec):
+        a = np.ascontiguousarray(rec, np.float32)
+        _ck(self.lib.ddrl_records_set(self.h, pid, a.ctypes.data, a.size))
+
+    def adv_norm_get(self, pid):
+        a = np.empty(2, np.float32)
+        _ck(self.lib.ddrl_adv_norm_get(self.h, pid, a.ctypes.data))
+        return a
+
+    def adv_norm_set(self, pid, mean, den):
+        _ck(self.lib.ddrl_adv_norm_set(self.h, pid, mean, den))
+
+    def last_values_get(self, pid):
+        a = np.empty(self.layout[pid]["C"], np.float32)
+        _ck(self.lib.ddrl_last_values_get(self.h, pid, a.ctypes.data, a.size))
+        return a
+
+    def done_set(self, done_tn):
+        a = np.ascontiguousarray(done_tn, np.uint8)
+        _ck(self.lib.ddrl_done_set(self.h, a.ctypes.data, a.size))
+
+    # ---- rollout ----
+    def observe(self, obs_dev):
+        _ck(self.lib.ddrl_observe(self.h, _ptr(obs_dev)))
+
+    def act(self, t, eps_dev, actions_dev):
+        _ck(self.lib.ddrl_act(self.h, t, _ptr(eps_dev), _ptr(actions_dev)))
+
+    def reward(self, t, fw_dev, cfrc_dev, actions_dev, done_dev=None):
+        _ck(self.lib.ddrl_reward(self.h, t, _ptr(fw_dev), _ptr(cfrc_dev), _ptr(actions_dev), _ptr(done_dev)))
+
+    def bootstrap(self):
+        _ck(self.lib.ddrl_bootstrap(self.h))
+
+    def step_host(self, t, obs_host, eps_host, actions_host):
+        _ck(self.lib.ddrl_step_host(self.h, t, _ptr(obs_host), _ptr(eps_host), _ptr(actions_host)))
+
+    def gae(self):
+        _ck(self.lib.ddrl_gae(self.h))
+
+    # ---- learner ----
+    def ppo_update(self, mask, shuffles, perms, kl_coeffs, max_steps=-1):
+        P = self.cfg.n_policies
+        sh = (VP * MAX_P)(*[_ptr(shuffles[p]) if shuffles[p] is not None else None for p in range(P)])
+        pe = (VP * MAX_P)(*[_ptr(perms[p]) if perms[p] is not None else None for p in range(P)])
+        kl = (f32 * MAX_P)(*[float(k) for k in kl_coeffs])
+        _ck(self.lib.ddrl_ppo_update(self.h, mask, sh, pe, kl, max_steps))
+
+    def ppo_stats(self, pid, n_steps):
+        a = np.empty((n_steps, 8), np.float32)
+        _ck(self.lib.ddrl_ppo_stats(self.h, pid, a.ctypes.data, n_steps))
+        return a
+
+    def ppo_grad(self, pid, rows_dev, n_rows, kl_coeff, grad_dev):
+        _ck(self.lib.ddrl_ppo_grad(self.h, pid, _ptr(rows_dev), n_rows, kl_coeff, _ptr(grad_dev)))
+
+    def ppo_apply(self, pid, grad_dev):
+        _ck(self.lib.ddrl_ppo_apply(self.h, pid, _ptr(grad_dev)))
+
+    def policy_forward(self, pid, obs_dev, n, logits_dev, values_dev, node_dev=None):
+        _ck(self.lib.ddrl_policy_forward(self.h, pid, _ptr(obs_dev), _ptr(node_dev), n,
+                                         _ptr(logits_dev), _ptr(values_dev)))

@@ -1,0 +1,80 @@
+"""Turn an env class + RLlib-style config into the C-ABI configuration (ddrl_cfg).
+
+Config keys follow train_experiment_1_architecture_on_flat.py:96-168 and the recorded
+params.json (gamma, lambda, clip_param, vf_clip_param, vf_loss_coeff, entropy_coeff, lr,
+grad_clip, sgd_minibatch_size, num_sgd_iter, rollout_fragment_length, env_config{...}).
+"""
+from __future__ import annotations
+
+from . import native as N
+from .simulation_envs import get_env_class
+
+PPO_DEFAULTS = {
+    # RLlib 1.0 PPO defaults as recorded in the reference's params.json, overridden by the
+    # exp-1 script (train_batch_size 16000, sgd_minibatch_size 128, lr 3e-4, grad_clip 0.5)
+    "gamma": 0.99, "lambda": 0.95, "clip_param": 0.2, "vf_clip_param": 10.0,
+    "vf_loss_coeff": 0.5, "entropy_coeff": 0.0, "kl_coeff": 0.2, "kl_target": 0.01,
+    "lr": 3e-4, "grad_clip": 0.5, "sgd_minibatch_size": 128, "num_sgd_iter": 10,
+    "train_batch_size": 16000, "rollout_fragment_length": 200, "shuffle_sequences": True,
+    "clip_actions": True, "vf_clip_mode": "ray10",
+}
+ENV_DEFAULTS = {"ctrl_cost_weight": 0.5, "contact_cost_weight": 5e-2, "hf_smoothness": 1.0,
+                "norm_reward": False, "global_reward": False, "filter_clip": 10.0,
+                "observation_filter_env": True}
+
+
+def make_cfg(env, n_envs, frag_len=None, config=None):
+    """env: registered name, class or instance.  Returns (DdrlCfg, env_instance)."""
+    config = {**PPO_DEFAULTS, **(config or {})}
+    env_config = {**ENV_DEFAULTS, **config.get("env_config", {})}
+    if isinstance(env, str):
+        env = get_env_class(env)
+    inst = env(env_config) if isinstance(env, type) else env
+    agents = list(inst.agent_names)
+    policies = list(type(inst).policy_names)
+    mapping = type(inst).policy_mapping_fn
+    c = N.DdrlCfg()
+    c.n_envs = int(n_envs)
+    c.frag_len = int(frag_len or config["rollout_fragment_length"])
+    c.obs_full_dim = len(inst.obs_fields)
+    c.n_agents = len(agents)
+    c.n_policies = len(policies)
+    c.model_kind = N.MODEL_GNN if inst.model_kind == "gnn" else N.MODEL_FFN
+    c.act_dim = len(inst.action_indices[agents[0]])
+    for j, a in enumerate(agents):
+        p = policies.index(mapping(a))
+        c.agent_policy[j] = p
+        idx = inst.obs_indices[a]
+        c.obs_dim[p] = len(idx)
+        for f, i in enumerate(idx):
+            c.obs_index[j][f] = i
+        for k, i in enumerate(inst.action_indices[a]):
+            c.act_index[j][k] = i
+        ci, cw = inst.contact_force_indices[a]
+        c.n_contact[j] = len(ci)
+        for k, (i, w) in enumerate(zip(ci, cw)):
+            c.contact_index[j][k] = i
+            c.contact_weight[j][k] = float(w[0] if isinstance(w, (list, tuple)) else w)
+    if inst.model_kind == "gnn":
+        for j, a in enumerate(agents):
+            c.leg_angle_deg[j] = inst.leg_angles[a]
+    c.filter_enabled = 1 if env_config.get("observation_filter_env", True) else 0
+    c.filter_update = 1
+    c.filter_clip = float(env_config.get("filter_clip", 10.0))
+    c.reward_mode = {"per_leg": N.REWARD_PER_LEG, "global": N.REWARD_GLOBAL,
+                     "norm": N.REWARD_NORM}[inst.reward_mode]
+    c.ctrl_cost_weight = float(env_config["ctrl_cost_weight"])
+    c.contact_cost_weight = float(env_config["contact_cost_weight"])
+    c.gamma = config["gamma"]
+    c.lambda_ = config["lambda"]
+    c.clip_param = config["clip_param"]
+    c.vf_clip_param = config["vf_clip_param"]
+    c.vf_loss_coeff = config["vf_loss_coeff"]
+    c.entropy_coeff = config["entropy_coeff"]
+    c.lr = config["lr"]
+    c.grad_clip = config["grad_clip"] if config["grad_clip"] is not None else 1e30
+    c.adam_beta1, c.adam_beta2, c.adam_eps = 0.9, 0.999, 1e-8
+    c.vf_clip_mode = N.VF_CLIP_RAY10 if config["vf_clip_mode"] == "ray10" else N.VF_CLIP_SQUARED
+    c.sgd_minibatch_size = int(config["sgd_minibatch_size"])
+    c.num_sgd_iter = int(config["num_sgd_iter"])
+    return c, inst

@@ -1,0 +1,168 @@
+/* ddrl_hip.h -- C-ABI of libddrl_hip.so, the MI355X (gfx950) hot path of DDRL.
+ *
+ * This boundary replaces the numeric work that the reference delegates to RLlib 1.0.x and
+ * TensorFlow 2.3, which run behind two plugin interfaces:
+ *   (1) MultiAgentEnv: simulation_envs/quantruped_adaptor_multi_environment.py:8-272
+ *       (distribute_observations :124-136, distribute_reward :173-203,
+ *        concatenate_actions :205-212, step :220-250)
+ *   (2) ModelV2: models/fcnet_glorot_uniform_init.py:10-125 ("ffn"),
+ *       models/shared_graphnet_glorot_uniform_init.py:14-58 + graph_net.py + gcn.py ("gnn"),
+ *       registered in models/__init__.py:7-13.
+ * The RLlib side they plug into (sampling, GAE, PPOLoss, clip_gradients, Adam, minibatch
+ * SGD, KL update) is rebuilt here as HIP kernels.  Host code -- Python through ctypes, or a
+ * maintainer's own FFI binding -- drives these entry points.
+ *
+ * Conventions
+ *   - Every function returns int status: 0 = OK, < 0 = error; ddrl_last_error() returns a
+ *     thread-local message.  No exceptions cross the boundary.
+ *   - Pointers named *_dev are device (HBM) pointers.  Pointers named *_host are host
+ *     memory (pageable or pinned).  Work is enqueued on the context's stream
+ *     (ddrl_set_stream) and is asynchronous unless stated otherwise.
+ *   - One context = one device + one stream; calls on a context are serialized by the caller.
+ */
+#ifndef DDRL_HIP_H
+#define DDRL_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DDRL_ABI_VERSION 1
+#define DDRL_MAX_POLICIES 4
+#define DDRL_MAX_AGENTS 4
+#define DDRL_MAX_OBS 48
+
+enum { DDRL_MODEL_FFN = 0, DDRL_MODEL_GNN = 1 };
+enum { DDRL_REWARD_PER_LEG = 0, DDRL_REWARD_GLOBAL = 1, DDRL_REWARD_NORM = 2 };
+enum { DDRL_VF_CLIP_RAY10 = 0, DDRL_VF_CLIP_SQUARED = 1 };
+
+/* Static configuration of one context (one env shard of one trainer). */
+typedef struct ddrl_cfg {
+  int32_t n_envs;        /* N: parallel environments on this device                      */
+  int32_t frag_len;      /* T: rollout_fragment_length                                     */
+  int32_t obs_full_dim;  /* 43 (44 with target velocity)                                   */
+  int32_t n_agents;      /* agents per env: 4 (legs), 2 (sides/diagonals), 1 (centralized) */
+  int32_t n_policies;    /* P                                                              */
+  int32_t model_kind;    /* DDRL_MODEL_FFN | DDRL_MODEL_GNN                               */
+  int32_t act_dim;       /* A: actions per agent (2, 4 or 8)                               */
+  int32_t agent_policy[DDRL_MAX_AGENTS];           /* policy id of every agent            */
+  int32_t obs_dim[DDRL_MAX_POLICIES];              /* d per policy (GNN: 19 per node)      */
+  int32_t obs_index[DDRL_MAX_AGENTS][DDRL_MAX_OBS];/* gather table per agent (a1)          */
+  int32_t act_index[DDRL_MAX_AGENTS][8];           /* scatter table per agent (a7)         */
+  int32_t n_contact[DDRL_MAX_AGENTS];              /* contact-cost bodies per agent (a8)   */
+  int32_t contact_index[DDRL_MAX_AGENTS][14];
+  float contact_weight[DDRL_MAX_AGENTS][14];
+  float leg_angle_deg[DDRL_MAX_AGENTS];            /* GNN ego encoding (FL,HL,HR,FR)       */
+  int32_t filter_enabled;   /* env-side MeanStdFilter on the full observation (a2)         */
+  int32_t filter_update;    /* push batches into the running statistics                   */
+  float filter_clip;        /* 10 in the reference; 0 = no clip                            */
+  int32_t reward_mode;      /* DDRL_REWARD_*                                                */
+  float ctrl_cost_weight;
+  float contact_cost_weight;
+  float gamma, lambda_;
+  float clip_param, vf_clip_param, vf_loss_coeff, entropy_coeff;
+  float lr, grad_clip;
+  float adam_beta1, adam_beta2, adam_eps;
+  int32_t vf_clip_mode;     /* DDRL_VF_CLIP_*                                               */
+  int32_t sgd_minibatch_size;  /* 128 (the fused update kernel is built for 128)          */
+  int32_t num_sgd_iter;        /* 10                                                       */
+} ddrl_cfg;
+
+typedef struct ddrl_ctx ddrl_ctx;
+
+int ddrl_abi_version(void);
+const char* ddrl_last_error(void);
+
+/* Context lifetime.  Allocates every device buffer for T x N rollouts. */
+int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out);
+int ddrl_ctx_destroy(ddrl_ctx* ctx);
+int ddrl_set_stream(ddrl_ctx* ctx, void* hip_stream);
+int ddrl_synchronize(ddrl_ctx* ctx);
+
+/* Shapes.  layout_out[10] = {row_stride, off_obs, off_act, off_logits, off_logp, off_vf,
+ * off_adv, off_vt, off_rew, rows_per_step (C = N*k)}, all in floats. */
+int ddrl_param_count(ddrl_ctx* ctx, int pid, int64_t* n_out);
+int ddrl_record_layout(ddrl_ctx* ctx, int pid, int32_t* layout_out);
+
+/* Parameter / optimizer / filter state, in the reference's Keras checkpoint order
+ * (pid/fc_1/kernel [d,64], fc_1/bias, fc_value_1/..., fc_2/..., fc_value_2/...,
+ *  fc_out/..., value_out/...), replacing Policy.get_weights/set_weights. */
+int ddrl_params_set(ddrl_ctx* ctx, int pid, const float* host, size_t n);
+int ddrl_params_get(ddrl_ctx* ctx, int pid, float* host, size_t n);
+int ddrl_adam_set(ddrl_ctx* ctx, int pid, const float* m_host, const float* v_host, size_t n,
+                  float beta1_power, float beta2_power);
+int ddrl_adam_get(ddrl_ctx* ctx, int pid, float* m_host, float* v_host, size_t n,
+                  float* beta1_power, float* beta2_power);
+int ddrl_filter_set(ddrl_ctx* ctx, double n, const double* mean_host, const double* sq_host);
+int ddrl_filter_get(ddrl_ctx* ctx, double* n, double* mean_host, double* sq_host);
+
+/* Rollout (per env step).
+ * observe: env-side MeanStdFilter push + normalize + per-agent routing of the raw
+ *          observations obs_dev[N][obs_full_dim] (a1/a2/a3).
+ * act:     fused forward of every policy on the routed observations, DiagGaussian sample
+ *          with explicit noise eps_dev[N][n_agents][A], logp, value; writes training row
+ *          t and the clipped env actions actions_dev[N][8] (a4/a6/a7).
+ * reward:  per-agent rewards for row t from forward reward fw_dev[N], contact forces
+ *          cfrc_dev[N][14][6], the env actions and done flags done_dev[N] (a8).
+ * bootstrap: V(s_T) of the routed observations -> last values for GAE. */
+int ddrl_observe(ddrl_ctx* ctx, const float* obs_dev);
+int ddrl_act(ddrl_ctx* ctx, int t, const float* eps_dev, float* actions_dev);
+int ddrl_reward(ddrl_ctx* ctx, int t, const float* fw_dev, const float* cfrc_dev,
+                const float* actions_dev, const uint8_t* done_dev);
+int ddrl_bootstrap(ddrl_ctx* ctx);
+/* Host-buffer variant of one env step (pinned buffers; hipMemcpyAsync in, actions out). */
+int ddrl_step_host(ddrl_ctx* ctx, int t, const float* obs_host, const float* eps_host,
+                   float* actions_host);
+
+/* Postprocessing: GAE over the fragment for every policy + advantage standardization
+ * statistics (a11/a12). */
+int ddrl_gae(ddrl_ctx* ctx);
+
+/* PPO update of policy pid_mask bits (a13-a17).  Per policy p (bit p set):
+ *   shuffle_dev[p] : int32[R_p] row permutation (SampleBatch.shuffle)
+ *   perm_dev[p]    : int32[num_sgd_iter][nb_p] minibatch-slot permutation per epoch,
+ *                    nb_p = max(1, R_p / sgd_minibatch_size)
+ *   kl_coeff[p]    : current KL coefficient
+ * max_steps < 0 runs the whole schedule; >= 0 runs only the first max_steps minibatches.
+ * All policies in the mask run concurrently (one persistent workgroup each). */
+int ddrl_ppo_update(ddrl_ctx* ctx, int pid_mask, const int32_t* const* shuffle_dev,
+                    const int32_t* const* perm_dev, const float* kl_coeff, int max_steps);
+/* Per-minibatch learner stats of the last update: n_steps x 8 floats
+ * {total_loss, policy_loss, vf_loss, kl, entropy, vf_explained_var, grad_gnorm, clip_scale}. */
+int ddrl_ppo_stats(ddrl_ctx* ctx, int pid, float* host, size_t n_steps);
+
+/* Data-parallel (shared policy) primitives: gradient of (1/minibatch) * sum over the
+ * given rows -> grad_dev[n_params]; after the caller's all-reduce (RCCL), apply clip +
+ * Adam.  rows_dev holds n_rows (<= 128) record indices. */
+int ddrl_ppo_grad(ddrl_ctx* ctx, int pid, const int32_t* rows_dev, int n_rows,
+                  float kl_coeff, float* grad_dev);
+int ddrl_ppo_apply(ddrl_ctx* ctx, int pid, const float* grad_dev);
+
+/* Model forward (ModelV2.forward + value_function) on arbitrary rows:
+ * obs_dev[n][d] (ffn) or X_dev[n][4][23] + node_dev[n] (gnn). */
+int ddrl_policy_forward(ddrl_ctx* ctx, int pid, const float* obs_dev, const int32_t* node_dev,
+                        int n, float* logits_dev, float* values_dev);
+
+/* Training-row buffers (SampleBatch columns) of policy pid, [T*C][row_stride] floats:
+ * read back for inspection, or loaded from an external batch (e.g. a replayed SampleBatch). */
+int ddrl_records_get(ddrl_ctx* ctx, int pid, float* host, size_t n_floats);
+int ddrl_records_set(ddrl_ctx* ctx, int pid, const float* host, size_t n_floats);
+/* Advantage standardization constants {mean, max(1e-4, std)} of policy pid. */
+int ddrl_adv_norm_get(ddrl_ctx* ctx, int pid, float* host2);
+int ddrl_adv_norm_set(ddrl_ctx* ctx, int pid, float mean, float denom);
+/* Bootstrap values V(s_T) of policy pid, C floats. */
+int ddrl_last_values_get(ddrl_ctx* ctx, int pid, float* host, size_t n);
+/* Episode-end flags of the fragment, [T][N] bytes (normally written by ddrl_reward). */
+int ddrl_done_set(ddrl_ctx* ctx, const uint8_t* host, size_t n);
+
+/* Direct device pointers (for zero-copy inspection and collectives). */
+int ddrl_device_buffers(ddrl_ctx* ctx, int pid, void** records, void** last_v, void** params,
+                        void** adv_norm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,181 @@
+"""Shared helpers for the GPU parity tests: build a context, run an oracle rollout on the
+same seeded inputs, and compare record buffers."""
+from __future__ import annotations
+
+import numpy as np
+
+from oracle import ddrl_oracle as O
+from ddrl_amd import native as N
+from ddrl_amd.spec import make_cfg
+
+
+def make_ctx(env, n_envs, T, config=None, stream=None):
+    import torch
+    cfg, inst = make_cfg(env, n_envs, T, config)
+    ctx = N.Context(cfg, 0, stream if stream is not None else torch.cuda.current_stream().cuda_stream)
+    return ctx, cfg, inst
+
+
+def policy_tables(cfg, inst):
+    """Per policy: list of (slot -> agent name) and d, from the cfg the kernels use."""
+    agents = list(inst.agent_names)
+    out = []
+    for p in range(cfg.n_policies):
+        slots = [a for j, a in enumerate(agents) if cfg.agent_policy[j] == p]
+        out.append(slots)
+    return out
+
+
+def init_params(ctx, cfg, seed, head_scale=30.0):
+    rng = np.random.default_rng(seed)
+    params = []
+    for p in range(cfg.n_policies):
+        A = cfg.act_dim
+        pr = O.ffn_init(rng, cfg.obs_dim[p], 2 * A)
+        pr["fc_out/kernel"] *= head_scale
+        pr["value_out/kernel"] *= head_scale
+        pr["fc_1/bias"] += rng.normal(size=64).astype(np.float32) * 0.1
+        pr["fc_out/bias"] += np.concatenate([np.zeros(A), -0.5 * np.ones(A)]).astype(np.float32)
+        shapes = O.ffn_param_shapes(cfg.obs_dim[p], 2 * A)
+        ctx.params_set(p, O.pack(pr, shapes))
+        params.append(pr)
+    return params
+
+
+class OracleRollout:
+    """Oracle restatement of observe/act/reward/bootstrap/GAE for a vectorized env."""
+
+    def __init__(self, cfg, inst, params, filt):
+        self.cfg, self.inst, self.params = cfg, inst, params
+        self.rs = O.RunningStat((cfg.obs_full_dim,))
+        self.rs.n, self.rs.M[:], self.rs.S[:] = filt
+        self.slots = policy_tables(cfg, inst)
+        self.agents = list(inst.agent_names)
+        T, N_ = cfg.frag_len, cfg.n_envs
+        self.rec = []
+        for p in range(cfg.n_policies):
+            C = N_ * len(self.slots[p])
+            self.rec.append(dict(obs=np.zeros((T, C, cfg.obs_dim[p]), np.float32),
+                                 act=np.zeros((T, C, cfg.act_dim), np.float32),
+                                 logits=np.zeros((T, C, 2 * cfg.act_dim), np.float32),
+                                 logp=np.zeros((T, C), np.float32), vf=np.zeros((T, C), np.float32),
+                                 rew=np.zeros((T, C), np.float32)))
+        self.done = np.zeros((T, N_), np.uint8)
+        self.stage = None
+
+    def observe(self, obs):
+        normed = O.mean_std_filter(obs, self.rs, update=True, clip=self.cfg.filter_clip)
+        self.stage = []
+        for p in range(self.cfg.n_policies):
+            cols = [normed[:, self.inst.obs_indices[a]] for a in self.slots[p]]
+            x = np.stack(cols, 1).reshape(-1, self.cfg.obs_dim[p])   # c = e * k + slot
+            self.stage.append(x.astype(np.float32))
+
+    def act(self, t, eps):
+        cfg = self.cfg
+        A = cfg.act_dim
+        actions = np.zeros((cfg.n_envs, 8), np.float32)
+        for p in range(cfg.n_policies):
+            x = self.stage[p]
+            logits, value, _ = O.ffn_forward(self.params[p], x)
+            k = len(self.slots[p])
+            e_idx = [self.agents.index(a) for a in self.slots[p]]
+            ep = eps[:, e_idx, :].reshape(-1, A)
+            a = O.dg_sample(logits, ep)
+            r = self.rec[p]
+            r["obs"][t], r["act"][t], r["logits"][t] = x, a, logits
+            r["logp"][t], r["vf"][t] = O.dg_logp(logits, a), value
+            for s, name in enumerate(self.slots[p]):
+                actions[:, self.inst.action_indices[name]] = np.clip(a.reshape(-1, k, A)[:, s], -1, 1)
+        return actions
+
+    def reward(self, t, fw, cfrc, actions, done):
+        cfg = self.cfg
+        for e in range(cfg.n_envs):
+            ad = {a: actions[e, self.inst.action_indices[a]].astype(np.float64) for a in self.agents}
+            tables = {a: (self.inst.contact_force_indices[a][0], self.inst.contact_force_indices[a][1])
+                      for a in self.agents}
+            if self.inst.reward_mode == "global":
+                rw = O.global_reward(float(fw[e]), cfrc[e].astype(np.float64), ad,
+                                     cfg.ctrl_cost_weight, cfg.contact_cost_weight)
+            else:
+                rw = O.per_leg_reward(float(fw[e]), cfrc[e].astype(np.float64), ad, tables,
+                                      cfg.ctrl_cost_weight, cfg.contact_cost_weight,
+                                      norm_reward=self.inst.reward_mode == "norm")
+            for p in range(cfg.n_policies):
+                k = len(self.slots[p])
+                for s, a in enumerate(self.slots[p]):
+                    self.rec[p]["rew"][t, e * k + s] = rw[a]
+        self.done[t] = done
+
+    def bootstrap(self):
+        self.last_v = [O.ffn_forward(self.params[p], self.stage[p])[1] for p in range(self.cfg.n_policies)]
+
+    def gae(self):
+        out = []
+        for p in range(self.cfg.n_policies):
+            k = len(self.slots[p])
+            dones = np.repeat(self.done, k, axis=1)
+            adv, vt = O.gae_fragment(self.rec[p]["rew"], self.rec[p]["vf"], dones, self.last_v[p],
+                                     self.cfg.gamma, self.cfg.lambda_)
+            self.rec[p]["adv"], self.rec[p]["vt"] = adv, vt
+            _, mean, std = O.standardize(adv.reshape(-1))
+            out.append((mean, max(np.float32(1e-4), std)))
+        return out
+
+    def flat_records(self, p, lay):
+        r = self.rec[p]
+        T, C = r["vf"].shape
+        out = np.zeros((T * C, lay["stride"]), np.float32)
+        d = r["obs"].shape[-1]
+        A = r["act"].shape[-1]
+        out[:, lay["obs"]:lay["obs"] + d] = r["obs"].reshape(T * C, d)
+        out[:, lay["act"]:lay["act"] + A] = r["act"].reshape(T * C, A)
+        out[:, lay["logit"]:lay["logit"] + 2 * A] = r["logits"].reshape(T * C, 2 * A)
+        for key, off in (("logp", "logp"), ("vf", "vf"), ("rew", "rew"), ("adv", "adv"), ("vt", "vt")):
+            if key in r:
+                out[:, lay[off]] = r[key].reshape(-1)
+        return out
+
+
+def synthetic_inputs(rng, cfg, T):
+    N_ = cfg.n_envs
+    obs = (rng.normal(size=(T + 1, N_, cfg.obs_full_dim)) * 2 + 0.5).astype(np.float32)
+    eps = rng.normal(size=(T, N_, cfg.n_agents, cfg.act_dim)).astype(np.float32)
+    fw = rng.normal(size=(T, N_)).astype(np.float32)
+    cfrc = (rng.normal(size=(T, N_, 14, 6)) * 1.5).astype(np.float32)
+    done = (rng.random(size=(T, N_)) < 0.05).astype(np.uint8)
+    return obs, eps, fw, cfrc, done
+
+
+def run_rollout(ctx, cfg, inst, params, rng, filt, T):
+    """Run the HIP rollout and the oracle on the same inputs; returns (oracle, inputs)."""
+    import torch
+    obs, eps, fw, cfrc, done = synthetic_inputs(rng, cfg, T)
+    ctx.filter_set(*filt)
+    orc = OracleRollout(cfg, inst, params, filt)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    actions = torch.zeros((cfg.n_envs, 8), dtype=torch.float32, device="cuda")
+    acts_gpu = []
+    acts_orc = []
+    for t in range(T):
+        o_t = dev(obs[t])
+        ctx.observe(o_t)
+        orc.observe(obs[t])
+        e_t = dev(eps[t])
+        ctx.act(t, e_t, actions)
+        a_orc = orc.act(t, eps[t])
+        acts_gpu.append(actions.cpu().numpy().copy())
+        acts_orc.append(a_orc)
+        f_t, c_t, d_t = dev(fw[t]), dev(cfrc[t]), dev(done[t])
+        # the env consumes the HIP actions; the oracle uses its own (compared separately)
+        ctx.reward(t, f_t, c_t, actions, d_t)
+        orc.reward(t, fw[t], cfrc[t], a_orc, done[t])
+    ctx.observe(dev(obs[T]))
+    orc.observe(obs[T])
+    ctx.bootstrap()
+    orc.bootstrap()
+    ctx.gae()
+    norms = orc.gae()
+    torch.cuda.synchronize()
+    return orc, norms, np.stack(acts_gpu), np.stack(acts_orc)

@@ -1,0 +1,223 @@
+"""HIP path vs CPU oracle through the C-ABI (needs an MI355X).
+
+Tolerances (fp32 path, float64 filter/GAE as in the reference):
+  * rollout outputs, rewards, GAE, gradients, losses: |gpu - ref| <= 1e-5 + 1e-5 |ref|
+    (gradients: relative to the tensor's max magnitude, see _close_grad)
+  * learner tests use the reference's own output-head scale (Glorot 0.01): with heads
+    scaled up 30x (used for the rollout tests) log_std gets small enough that the loss is
+    ill-conditioned and fp32 summation-order differences reach 2e-4 relative
+  * parameters after Adam steps: 1e-5 absolute for >= 99.9 % of the entries; the rest
+    (gradients within rounding of zero, where Adam's m / sqrt(v) flips sign) within
+    2 * lr per step.
+"""
+import numpy as np
+import pytest
+
+from oracle import ddrl_oracle as O
+from tests.gpu_harness import init_params, make_ctx, run_rollout
+
+pytestmark = pytest.mark.gpu
+RT, AT = 1e-5, 1e-5
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ddrl_amd import build
+    build.build()
+
+
+def _close(a, b, rtol=RT, atol=AT, msg=""):
+    np.testing.assert_allclose(a, b, rtol=rtol, atol=atol, err_msg=msg)
+
+
+def _filt(D, rng):
+    return (1000.0, rng.normal(size=D) * 0.3, np.abs(rng.normal(size=D)) * 999.0 + 10.0)
+
+
+ROLLOUT_ENVS = [
+    ("QuantrupedMultiEnv_Local", 64, 6),
+    ("QuantrupedMultiEnv_FullyDecentral", 40, 5),
+    ("QuantrupedMultiEnv_SharedDecentral", 33, 5),
+    ("QuantrupedMultiEnv_Centralized", 50, 4),
+    ("QuantrupedMultiEnv_TwoSides", 20, 4),
+]
+
+
+@pytest.mark.parametrize("env,n,T", ROLLOUT_ENVS)
+def test_rollout_gae_parity(env, n, T):
+    ctx, cfg, inst = make_ctx(env, n, T)
+    rng = np.random.default_rng(11)
+    params = init_params(ctx, cfg, 3)
+    orc, norms, a_gpu, a_orc = run_rollout(ctx, cfg, inst, params, rng, _filt(cfg.obs_full_dim, rng), T)
+    _close(a_gpu, a_orc, msg="env actions")
+    fn, fM, fS = ctx.filter_get()
+    assert fn == orc.rs.n
+    _close(fM, orc.rs.M, rtol=1e-12, atol=1e-12)
+    _close(fS, orc.rs.S, rtol=1e-10, atol=1e-9)
+    for p in range(cfg.n_policies):
+        lay = ctx.layout[p]
+        got = ctx.records_get(p)
+        ref = orc.flat_records(p, lay)
+        d, A = cfg.obs_dim[p], cfg.act_dim
+        for name, sl in [("obs", slice(lay["obs"], lay["obs"] + d)),
+                         ("act", slice(lay["act"], lay["act"] + A)),
+                         ("logits", slice(lay["logit"], lay["logit"] + 2 * A)),
+                         ("logp", lay["logp"]), ("vf", lay["vf"]), ("rew", lay["rew"]),
+                         ("adv", lay["adv"]), ("vt", lay["vt"])]:
+            _close(got[:, sl], ref[:, sl], rtol=1e-5, atol=2e-5, msg=f"{env} p{p} {name}")
+        _close(ctx.last_values_get(p), orc.last_v[p], msg="bootstrap V(s_T)")
+        an = ctx.adv_norm_get(p)
+        _close(an, np.array(norms[p], np.float32), rtol=1e-5, atol=1e-6, msg="adv mean/std")
+    ctx.close()
+
+
+def _batch_from_records(rec, lay, d, A, adv_norm):
+    mean, den = adv_norm
+    return dict(obs=rec[:, lay["obs"]:lay["obs"] + d], actions=rec[:, lay["act"]:lay["act"] + A],
+                logits=rec[:, lay["logit"]:lay["logit"] + 2 * A], logp=rec[:, lay["logp"]],
+                vf_preds=rec[:, lay["vf"]], adv=((rec[:, lay["adv"]] - mean) / den).astype(np.float32),
+                vt=rec[:, lay["vt"]])
+
+
+def _params_close(got, ref, lr, steps, msg):
+    diff = np.abs(got - ref)
+    frac = np.mean(diff <= 1e-5 + 1e-5 * np.abs(ref))
+    assert frac >= 0.999, f"{msg}: only {frac:.5f} of params within 1e-5 (max {diff.max():.3g})"
+    assert diff.max() <= 2 * lr * steps + 1e-5, f"{msg}: max deviation {diff.max():.3g}"
+
+
+@pytest.mark.parametrize("env,n,T,steps", [
+    ("QuantrupedMultiEnv_Local", 64, 6, 3),
+    ("QuantrupedMultiEnv_SharedDecentral", 32, 4, 2),
+    ("QuantrupedMultiEnv_Centralized", 48, 8, 2),
+])
+def test_ppo_update_parity(env, n, T, steps):
+    import torch
+    ctx, cfg, inst = make_ctx(env, n, T)
+    rng = np.random.default_rng(5)
+    params = init_params(ctx, cfg, 7, head_scale=1.0)
+    orc, norms, _, _ = run_rollout(ctx, cfg, inst, params, rng, _filt(cfg.obs_full_dim, rng), T)
+    shuffles, perms, kls = [], [], []
+    for p in range(cfg.n_policies):
+        lay = ctx.layout[p]
+        # feed the ORACLE's batch so the update parity does not inherit rollout rounding
+        ctx.records_set(p, orc.flat_records(p, lay))
+        ctx.adv_norm_set(p, *norms[p])
+        R = T * lay["C"]
+        sh, pe = O.sgd_schedule(np.random.default_rng(100 + p), R, 128, cfg.num_sgd_iter)
+        shuffles.append(sh)
+        perms.append(pe)
+        kls.append(0.2 + 0.1 * p)
+    dsh = [torch.from_numpy(s).cuda() for s in shuffles]
+    dpe = [torch.from_numpy(s).cuda() for s in perms]
+    ctx.ppo_update((1 << cfg.n_policies) - 1, dsh, dpe, kls, max_steps=steps)
+    ctx.synchronize()
+    for p in range(cfg.n_policies):
+        lay = ctx.layout[p]
+        d, A = cfg.obs_dim[p], cfg.act_dim
+        batch = _batch_from_records(orc.flat_records(p, lay), lay, d, A, norms[p])
+        shapes = O.ffn_param_shapes(d, 2 * A)
+        adam = O.Adam(sum(int(np.prod(s)) for _, s in shapes), lr=cfg.lr)
+        new, stats = O.ppo_update("ffn", params[p], shapes, adam, batch, shuffles[p], perms[p],
+                                  np.float32(kls[p]), {"entropy_coeff": 0.0}, steps=steps)
+        got = ctx.params_get(p)
+        _params_close(got, O.pack(new, shapes), cfg.lr, steps, f"{env} p{p}")
+        m, v, b1p, b2p = ctx.adam_get(p)
+        assert b1p == np.float32(adam.b1p) and b2p == np.float32(adam.b2p)
+        st = ctx.ppo_stats(p, steps)
+        for k, s in enumerate(stats):
+            ref = [s["total_loss"], s["policy_loss"], s["vf_loss"], s["kl"], s["entropy"],
+                   s["vf_explained_var"], s["grad_gnorm"]]
+            _close(st[k, :7], np.array(ref, np.float32), rtol=1e-4, atol=1e-5, msg=f"stats step {k}")
+    ctx.close()
+
+
+def test_full_schedule_runs_and_stays_close():
+    """Whole schedule (10 epochs x nb minibatches) for the Local config."""
+    import torch
+    env, n, T = "QuantrupedMultiEnv_Local", 64, 4   # R = 256 rows, nb = 2, 20 steps
+    ctx, cfg, inst = make_ctx(env, n, T)
+    rng = np.random.default_rng(9)
+    params = init_params(ctx, cfg, 2, head_scale=1.0)
+    orc, norms, _, _ = run_rollout(ctx, cfg, inst, params, rng, _filt(cfg.obs_full_dim, rng), T)
+    sh, pe = O.sgd_schedule(np.random.default_rng(1), T * n, 128, 10)
+    for p in range(4):
+        ctx.records_set(p, orc.flat_records(p, ctx.layout[p]))
+        ctx.adv_norm_set(p, *norms[p])
+    dsh = [torch.from_numpy(sh).cuda()] * 4
+    dpe = [torch.from_numpy(pe).cuda()] * 4
+    ctx.ppo_update(0xF, dsh, dpe, [0.2] * 4)
+    ctx.synchronize()
+    p = 1
+    lay = ctx.layout[p]
+    batch = _batch_from_records(orc.flat_records(p, lay), lay, 35, 2, norms[p])
+    shapes = O.ffn_param_shapes(35, 4)
+    adam = O.Adam(sum(int(np.prod(s)) for _, s in shapes))
+    new, stats = O.ppo_update("ffn", params[p], shapes, adam, batch, sh, pe, np.float32(0.2), {})
+    got = ctx.params_get(p)
+    ref = O.pack(new, shapes)
+    diff = np.abs(got - ref)
+    assert np.mean(diff <= 1e-4) >= 0.999 and diff.max() <= 2 * 3e-4 * 20
+    st = ctx.ppo_stats(p, 20)
+    _close(st[-1, 0], stats[-1]["total_loss"], rtol=1e-3, atol=1e-4)
+    ctx.close()
+
+
+def test_ddp_grad_and_apply_match_fused_step():
+    """Gradient of two 64-row halves summed == 128-row gradient; apply == fused step."""
+    import torch
+    env, n, T = "QuantrupedMultiEnv_SharedDecentral", 32, 4
+    ctx, cfg, inst = make_ctx(env, n, T)
+    rng = np.random.default_rng(4)
+    params = init_params(ctx, cfg, 8, head_scale=1.0)
+    orc, norms, _, _ = run_rollout(ctx, cfg, inst, params, rng, _filt(cfg.obs_full_dim, rng), T)
+    lay = ctx.layout[0]
+    ctx.records_set(0, orc.flat_records(0, lay))
+    ctx.adv_norm_set(0, *norms[0])
+    rows = np.random.default_rng(3).permutation(T * lay["C"])[:128].astype(np.int32)
+    npar = ctx.n_params[0]
+    g_full = torch.zeros(npar, device="cuda")
+    g_a = torch.zeros(npar, device="cuda")
+    g_b = torch.zeros(npar, device="cuda")
+    r_all = torch.from_numpy(rows).cuda()
+    ctx.ppo_grad(0, r_all, 128, 0.2, g_full)
+    ctx.ppo_grad(0, r_all[:64].contiguous(), 64, 0.2, g_a)
+    ctx.ppo_grad(0, r_all[64:].contiguous(), 64, 0.2, g_b)
+    ctx.synchronize()
+    gf = g_full.cpu().numpy()
+    gs = (g_a + g_b).cpu().numpy()
+    np.testing.assert_allclose(gs, gf, rtol=1e-4, atol=1e-6 * np.abs(gf).max())
+    # oracle gradient of the same rows
+    batch = _batch_from_records(orc.flat_records(0, lay), lay, 19, 2, norms[0])
+    sl = {k: v[rows] for k, v in batch.items()}
+    logits, value, cache = O.ffn_forward(params[0], sl["obs"])
+    dl, dv, _ = O.ppo_loss_rows(logits, value, sl["actions"], sl["logits"], sl["logp"],
+                                sl["vf_preds"], sl["adv"], sl["vt"], np.float32(0.2))
+    shapes = O.ffn_param_shapes(19, 4)
+    gref = O.pack(O.ffn_backward(params[0], cache, dl, dv), shapes)
+    np.testing.assert_allclose(gf, gref, rtol=1e-4, atol=2e-5 * np.abs(gref).max())
+    ctx.ppo_apply(0, g_full)
+    ctx.synchronize()
+    adam = O.Adam(npar)
+    clipped, _ = O.clip_by_global_norm([gref], 0.5)
+    ref = adam.apply(O.pack(params[0], shapes), clipped[0])
+    _params_close(ctx.params_get(0), ref, 3e-4, 1, "ddp apply")
+    ctx.close()
+
+
+def test_policy_forward_matches_oracle():
+    import torch
+    ctx, cfg, inst = make_ctx("QuantrupedMultiEnv_Local", 8, 2)
+    params = init_params(ctx, cfg, 21)
+    x = np.random.default_rng(0).normal(size=(203, 35)).astype(np.float32)
+    logits = torch.zeros((203, 4), device="cuda")
+    values = torch.zeros(203, device="cuda")
+    ctx.policy_forward(2, torch.from_numpy(x).cuda(), 203, logits, values)
+    ctx.synchronize()
+    lr, vr, _ = O.ffn_forward(params[2], x)
+    _close(logits.cpu().numpy(), lr)
+    _close(values.cpu().numpy(), vr)
+    ctx.close()
