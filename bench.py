@@ -1,0 +1,254 @@
+"""DDRL rollout + multi-agent PPO update on MI355X: env-steps/s at 4096 envs x 4 leg agents.
+
+One bench step = one PPO training iteration of the reference's exp-1 trainer on the
+QuantrupedMultiEnv_Local configuration (4 independent per-leg fcnet 2x64 policies, d = 35):
+  rollout of rollout_fragment_length = 200 vector env-steps over this rank's envs
+    (env-side MeanStdFilter + routing, fused forward of the 4 policies + DiagGaussian
+     sampling, per-leg rewards; synthetic QuAntruped data resident in HBM),
+  bootstrap V(s_T), GAE + advantage standardization,
+  SampleBatch shuffle + per-epoch minibatch permutations,
+  PPO update: num_sgd_iter = 10 epochs x (R / 128) minibatches per policy, all 4 policies
+    concurrently (fused persistent kernel: forward, PPOLoss, backward, clip, Adam),
+  KL-coefficient update from the last epoch's mean KL (host).
+Multi-GPU: 4096 envs are sharded over the ranks (C3: independent policies, no collective);
+each rank is an independent learner on its shard ("replicas"), value = all ranks' env-steps
+divided by the slowest rank's time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 4096] [--no-cpu-baseline]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env-steps/sec at 4096 envs × 4 leg agents; PPO update ms/minibatch"
+PEAK_FP32_TFLOPS = 157.3   # MI355X dense FP32 (MFMA f32 = vector rate), MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+
+
+def ffn_flops_per_row(d, A, H=64):
+    """Algorithmic FLOPs of one minibatch row through the fused update step:
+    forward (policy + value) + input-gradient backward of layers 2/head + weight gradients."""
+    fwd = d * H + H * H + H * 2 * A + d * H + H * H + H * 1
+    dx = (H * H + H * 2 * A) + (H * H + H * 1)
+    return 2 * (2 * fwd + dx)
+
+
+def ffn_fwd_flops_per_row(d, A, H=64):
+    return 2 * (d * H + H * H + H * 2 * A + d * H + H * H + H)
+
+
+def cpu_baseline(env, n_envs=128, T=200, seed=0):
+    """The numpy oracle on a bounded sample of the same workload (same env, same PPO
+    schedule, fewer envs), BLAS limited to one thread.  Returns env-steps/s."""
+    from threadpoolctl import threadpool_limits
+    from oracle import ddrl_oracle as O
+    from ddrl_amd.spec import make_cfg
+    cfg, inst = make_cfg(env, n_envs, T)
+    rng = np.random.default_rng(seed)
+    P, A = cfg.n_policies, cfg.act_dim
+    agents = list(inst.agent_names)
+    params = [O.ffn_init(rng, cfg.obs_dim[p], 2 * A) for p in range(P)]
+    shapes = [O.ffn_param_shapes(cfg.obs_dim[p], 2 * A) for p in range(P)]
+    obs = rng.normal(size=(T + 1, n_envs, cfg.obs_full_dim)).astype(np.float32)
+    eps = rng.normal(size=(T, n_envs, cfg.n_agents, A)).astype(np.float32)
+    fw = rng.normal(size=(T, n_envs)).astype(np.float32)
+    cfrc = rng.normal(size=(T, n_envs, 14, 6)).astype(np.float32)
+    with threadpool_limits(limits=1):
+        t0 = time.perf_counter()
+        rs = O.RunningStat((cfg.obs_full_dim,))
+        rec = [dict(obs=[], act=[], logits=[], logp=[], vf=[]) for _ in range(P)]
+        rew = np.zeros((P, T, n_envs), np.float32)
+        tables = {a: inst.contact_force_indices[a] for a in agents}
+        z = O.mean_std_filter(obs[0], rs, True, 10.0)
+        for t in range(T):
+            actions = np.zeros((n_envs, 8))
+            for p in range(P):
+                a_name = agents[p]
+                x = z[:, inst.obs_indices[a_name]].astype(np.float32)
+                logits, value, _ = O.ffn_forward(params[p], x)
+                act = O.dg_sample(logits, eps[t, :, p])
+                for k, v in (("obs", x), ("act", act), ("logits", logits),
+                             ("logp", O.dg_logp(logits, act)), ("vf", value)):
+                    rec[p][k].append(v)
+                actions[:, inst.action_indices[a_name]] = np.clip(act, -1, 1)
+            for e in range(n_envs):
+                ad = {a: actions[e, inst.action_indices[a]] for a in agents}
+                rw = O.per_leg_reward(float(fw[t, e]), cfrc[t, e], ad, tables, 0.5, 0.05)
+                for p in range(P):
+                    rew[p, t, e] = rw[agents[p]]
+            z = O.mean_std_filter(obs[t + 1], rs, True, 10.0)
+        for p in range(P):
+            r = {k: np.stack(v) for k, v in rec[p].items()}
+            r["rew"] = rew[p]
+            last_v = O.ffn_forward(params[p], z[:, inst.obs_indices[agents[p]]].astype(np.float32))[1]
+            adv, vt = O.gae_fragment(r["rew"], r["vf"], np.zeros((T, n_envs), bool), last_v)
+            adv, _, _ = O.standardize(adv.reshape(-1))
+            R = T * n_envs
+            batch = dict(obs=r["obs"].reshape(R, -1), actions=r["act"].reshape(R, -1),
+                         logits=r["logits"].reshape(R, -1), logp=r["logp"].reshape(-1),
+                         vf_preds=r["vf"].reshape(-1), adv=adv, vt=vt.reshape(-1))
+            sh, pe = O.sgd_schedule(rng, R, 128, 10)
+            adam = O.Adam(sum(int(np.prod(s)) for _, s in shapes[p]))
+            O.ppo_update("ffn", params[p], shapes[p], adam, batch, sh, pe, np.float32(0.2), {})
+        dt = time.perf_counter() - t0
+    return T * n_envs / dt, dt, f"{env}: {n_envs} envs x T={T} (full iteration: rollout, GAE, " \
+                                f"10 x {T * n_envs // 128} minibatches x {P} policies)"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--envs", type=int, default=4096, help="total envs over all ranks")
+    ap.add_argument("--env", default="QuantrupedMultiEnv_Local")
+    ap.add_argument("--frag", type=int, default=200)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-envs", type=int, default=128)
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from ddrl_amd import native as N
+    from ddrl_amd.build import build
+    from ddrl_amd.spec import make_cfg
+    from ddrl_amd.synthetic import SyntheticRollout
+    if rank == 0 and not os.path.exists(N.LIB_PATH):
+        build()
+    if dist is not None:
+        dist.barrier()
+
+    n_local = args.envs // world + (1 if rank < args.envs % world else 0)
+    T = args.frag
+    cfg, inst = make_cfg(args.env, n_local, T)
+    stream = torch.cuda.current_stream()
+    ctx = N.Context(cfg, local, stream.cuda_stream)
+    rng = np.random.default_rng(1234 + rank)
+    from ddrl_amd.trainer import glorot_ffn_flat
+    P, A = cfg.n_policies, cfg.act_dim
+    for p in range(P):
+        ctx.params_set(p, glorot_ffn_flat(rng, cfg.obs_dim[p], A))
+    syn = SyntheticRollout(n_local, T, cfg.obs_full_dim, cfg.n_agents, A, f"cuda:{local}", seed=rank)
+    kl = [0.2] * P
+    R = [T * ctx.layout[p]["C"] for p in range(P)]
+    nb = [max(1, r // 128) for r in R]
+    E = cfg.num_sgd_iter
+    gen = torch.Generator(device=f"cuda:{local}")
+    gen.manual_seed(99 + rank)
+    ev_upd = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    upd_ms = []
+
+    ctx.observe(syn.obs[0])
+
+    def iteration(record):
+        done = syn.dones_for_fragment()
+        for t in range(T):
+            ctx.act(t, syn.eps[t], syn.actions)
+            ctx.reward(t, syn.fw[t], syn.cfrc[t], syn.actions, done[t])
+            ctx.observe(syn.obs[t + 1])
+        ctx.bootstrap()
+        ctx.gae()
+        shuffles = [torch.randperm(R[p], device=stream.device, generator=gen, dtype=torch.int32) for p in range(P)]
+        perms = [torch.stack([torch.randperm(nb[p], device=stream.device, generator=gen, dtype=torch.int32)
+                              for _ in range(E)]).contiguous() for p in range(P)]
+        ev_upd[0].record(stream)
+        ctx.ppo_update((1 << P) - 1, shuffles, perms, kl)
+        ev_upd[1].record(stream)
+        # RLlib: update_kl with the last epoch's mean KL of every policy
+        for p in range(P):
+            st = ctx.ppo_stats(p, E * nb[p])
+            mkl = float(np.mean(st[-nb[p]:, 3]))
+            kl[p] = kl[p] * 1.5 if mkl > 2 * 0.01 else (kl[p] * 0.5 if mkl < 0.5 * 0.01 else kl[p])
+        if record:
+            upd_ms.append(ev_upd[0].elapsed_time(ev_upd[1]))
+
+    for _ in range(args.warmup):
+        iteration(False)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        iteration(True)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t_max = elapsed
+    env_steps = T * n_local * args.steps
+    if dist is not None:
+        tt = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+        es = torch.tensor([env_steps], device="cuda", dtype=torch.float64)
+        dist.all_reduce(es)
+        env_steps = int(es.item())
+
+    upd_avg_ms = float(np.mean(upd_ms))
+    steps_per_policy = E * nb[0]
+    mb_latency_ms = upd_avg_ms / steps_per_policy                 # one policy's sequential step
+    mb_amortized_ms = upd_avg_ms / (steps_per_policy * P)        # reference's learn_time / (P*10*nb)
+    d = cfg.obs_dim[0]
+    flops_launch = ffn_flops_per_row(d, A) * 128 * steps_per_policy * P
+    achieved_tf = flops_launch / (upd_avg_ms * 1e-3) / 1e12
+    result = {
+        "metric": METRIC,
+        "value": env_steps / t_max,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": t_max / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic QuAntruped rollouts resident in HBM (no MuJoCo); Glorot-init weights",
+        "config": {
+            "workload": f"{args.env}: {args.envs} envs x {cfg.n_agents} leg agents, {P} independent "
+                        f"fcnet 2x64 policies (d={d}, A={A}), T={T}, train batch {R[0]} rows/policy, "
+                        f"{E} epochs x {nb[0]} minibatches x 128",
+            "envs_total": args.envs, "envs_per_gpu": n_local, "parallelism": "replicas (no collective)",
+        },
+        "ppo_update_ms_per_minibatch": mb_amortized_ms,
+        "ppo_update_ms_per_minibatch_latency": mb_latency_ms,
+        "update_kernel_ms": upd_avg_ms,
+        "roofline": {
+            "kernel": "k_update_ffn (fused PPO minibatch SGD, one launch per iteration)",
+            "bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": None,
+            "algorithmic_flops_per_launch": flops_launch,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        v, dt, sample = cpu_baseline(args.env, args.cpu_envs, T)
+        result["cpu_baseline"] = {"value": v, "unit": "env-steps/s", "cores": 1, "kind": "port",
+                                  "sample": sample + f"; {dt:.1f} s", "host_cpus": os.cpu_count()}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

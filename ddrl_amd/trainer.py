@@ -1,0 +1,210 @@
+"""PPO trainer over the HIP hot path -- the drop-in for train_experiment_1's tune.run("PPO").
+
+Reference call stack: RLlib PPOTrainer with ParallelRollouts ->
+postprocess_ppo_gae -> StandardizeFields(["advantages"]) -> TrainTFMultiGPU (num_sgd_iter
+epochs over R // sgd_minibatch_size shuffled minibatches per policy) -> update_kl.
+Here one `train()` call is one training iteration: T = rollout_fragment_length vector env
+steps on the device, bootstrap + GAE on the device, then one fused persistent update launch
+for all policies (or, for a shared policy across ranks, per-minibatch gradient all-reduce).
+
+The config dict uses the reference's keys (train_experiment_1_architecture_on_flat.py:96-168).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import time
+
+import numpy as np
+
+from . import native as N
+from .spec import PPO_DEFAULTS, make_cfg
+
+
+def glorot_ffn_flat(rng, d, A, hidden=64):
+    """GlorotUniformScaled init (models/glorot_uniform_scaled_initializer.py:3-19): hidden
+    kernels scale 1.0, fc_out / value_out scale 0.01, biases 0; Keras flat order."""
+    def g(fi, fo, s):
+        lim = math.sqrt(6.0 * s / (fi + fo))
+        return rng.uniform(-lim, lim, size=(fi, fo)).astype(np.float32)
+    z = lambda n: np.zeros(n, np.float32)
+    parts = [g(d, hidden, 1.0), z(hidden), g(d, hidden, 1.0), z(hidden),
+             g(hidden, hidden, 1.0), z(hidden), g(hidden, hidden, 1.0), z(hidden),
+             g(hidden, 2 * A, 0.01), z(2 * A), g(hidden, 1, 0.01), z(1)]
+    return np.concatenate([p.reshape(-1) for p in parts])
+
+
+class PPOTrainer:
+    """Multi-agent PPO on one device (one env shard).
+
+    env_backend: an object with reset() -> obs[N, D] (device tensor) and
+    step(actions[N, 8]) -> (obs_next, fw[N], cfrc[N, 14, 6], done[N] uint8); defaults to the
+    synthetic vectorized QuAntruped (`ddrl_amd.envs.SyntheticVecEnv`).
+    """
+
+    def __init__(self, config, n_envs=None, device=0, env_backend=None, seed=0, stream=None):
+        import torch
+        self.torch = torch
+        self.config = {**PPO_DEFAULTS, **config}
+        c = self.config
+        env = c["env"]
+        self.n_envs = int(n_envs or c.get("num_envs", c.get("num_workers", 2) * c.get("num_envs_per_worker", 4)))
+        self.T = int(c["rollout_fragment_length"])
+        self.cfg, self.env = make_cfg(env, self.n_envs, self.T, c)
+        torch.cuda.set_device(device)
+        self.device = torch.device("cuda", device)
+        self.stream = stream or torch.cuda.current_stream(self.device)
+        self.ctx = N.Context(self.cfg, device, self.stream.cuda_stream)
+        self.policy_ids = list(type(self.env).policy_names)
+        P = self.cfg.n_policies
+        self.rng = np.random.default_rng(seed)
+        for p in range(P):
+            if self.cfg.model_kind == N.MODEL_FFN:
+                self.ctx.params_set(p, glorot_ffn_flat(self.rng, self.cfg.obs_dim[p], self.cfg.act_dim))
+            else:
+                from .models import glorot_gnn_flat
+                self.ctx.params_set(p, glorot_gnn_flat(self.rng, self.cfg.act_dim))
+        self.kl_coeff = [float(c["kl_coeff"])] * P
+        if env_backend is None:
+            from .envs import SyntheticVecEnv
+            env_backend = SyntheticVecEnv(self.n_envs, self.cfg.obs_full_dim, self.device, seed=seed)
+        self.backend = env_backend
+        self.actions = torch.zeros((self.n_envs, 8), dtype=torch.float32, device=self.device)
+        self.noise_gen = torch.Generator(device=self.device)
+        self.noise_gen.manual_seed(seed + 1)
+        self.timesteps_total = 0
+        self.iteration = 0
+        self.ctx.observe(self.backend.reset())
+
+    # -- one iteration ---------------------------------------------------------------
+    def _sample(self):
+        torch, cfg = self.torch, self.cfg
+        for t in range(self.T):
+            eps = torch.randn((self.n_envs, cfg.n_agents, cfg.act_dim), device=self.device,
+                              generator=self.noise_gen)
+            self.ctx.act(t, eps, self.actions)
+            obs, fw, cfrc, done = self.backend.step(self.actions)
+            self.ctx.reward(t, fw, cfrc, self.actions, done)
+            self.ctx.observe(obs)
+        self.ctx.bootstrap()
+        self.ctx.gae()
+
+    def _schedule(self, p):
+        """SampleBatch.shuffle() + one permutation of the minibatch slots per epoch."""
+        R = self.T * self.ctx.layout[p]["C"]
+        mb = self.cfg.sgd_minibatch_size
+        shuffle = self.rng.permutation(R).astype(np.int32)
+        nb = max(1, R // mb)
+        perms = np.stack([self.rng.permutation(nb) for _ in range(self.cfg.num_sgd_iter)]).astype(np.int32)
+        return shuffle, perms, nb
+
+    def _learn(self):
+        torch = self.torch
+        P = self.cfg.n_policies
+        sh, pe, nbs = [], [], []
+        for p in range(P):
+            s, q, nb = self._schedule(p)
+            sh.append(torch.from_numpy(s).to(self.device))
+            pe.append(torch.from_numpy(q).to(self.device))
+            nbs.append(nb)
+        self.ctx.ppo_update((1 << P) - 1, sh, pe, self.kl_coeff)
+        learner = {}
+        for p, pid in enumerate(self.policy_ids):
+            st = self.ctx.ppo_stats(p, self.cfg.num_sgd_iter * nbs[p])
+            last = st[-nbs[p]:].astype(np.float64).mean(0)   # TrainTFMultiGPU: last epoch's mean
+            learner[pid] = {"cur_kl_coeff": float(np.float32(self.kl_coeff[p])),
+                            "cur_lr": float(np.float32(self.cfg.lr)),
+                            "total_loss": last[0], "policy_loss": last[1], "vf_loss": last[2],
+                            "kl": last[3], "entropy": last[4], "vf_explained_var": last[5],
+                            "grad_gnorm": last[6], "entropy_coeff": self.cfg.entropy_coeff}
+            self.kl_coeff[p] = update_kl(self.kl_coeff[p], last[3], self.config["kl_target"])
+        return learner
+
+    def train(self):
+        torch = self.torch
+        t0 = time.perf_counter()
+        self._sample()
+        torch.cuda.synchronize(self.device)
+        t1 = time.perf_counter()
+        learner = self._learn()
+        t2 = time.perf_counter()
+        steps = self.T * self.n_envs
+        self.timesteps_total += steps
+        self.iteration += 1
+        cb = self.config.get("callbacks", {}).get("on_train_result") if isinstance(
+            self.config.get("callbacks"), dict) else None
+        result = {"training_iteration": self.iteration, "timesteps_total": self.timesteps_total,
+                  "timesteps_this_iter": steps, "info": {"learner": learner},
+                  "timers": {"sample_time_ms": (t1 - t0) * 1e3, "learn_time_ms": (t2 - t1) * 1e3,
+                             "sample_throughput": steps / (t1 - t0),
+                             "learn_throughput": steps / (t2 - t1)}}
+        if cb:
+            cb({"result": result, "trainer": self})
+        return result
+
+    # -- state -------------------------------------------------------------------------
+    def get_weights(self):
+        return {pid: self.ctx.params_get(p) for p, pid in enumerate(self.policy_ids)}
+
+    def set_weights(self, weights):
+        for p, pid in enumerate(self.policy_ids):
+            if pid in weights:
+                self.ctx.params_set(p, weights[pid])
+
+    def save(self, path):
+        """Checkpoint: weights, Adam m/v/beta powers, KL coefficients, filter state (npz,
+        no pickle)."""
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        arrs = {}
+        for p, pid in enumerate(self.policy_ids):
+            m, v, b1, b2 = self.ctx.adam_get(p)
+            arrs[f"{pid}/weights"] = self.ctx.params_get(p)
+            arrs[f"{pid}/adam_m"], arrs[f"{pid}/adam_v"] = m, v
+            arrs[f"{pid}/beta_powers"] = np.array([b1, b2], np.float32)
+            arrs[f"{pid}/kl_coeff"] = np.array([self.kl_coeff[p]])
+        n, M, S = self.ctx.filter_get()
+        arrs["filter/n"], arrs["filter/M"], arrs["filter/S"] = np.array([n]), M, S
+        arrs["meta"] = np.frombuffer(json.dumps({"iteration": self.iteration,
+                                                 "timesteps_total": self.timesteps_total}).encode(), np.uint8)
+        np.savez(path, **arrs)
+        return path
+
+    def restore(self, path):
+        z = np.load(path, allow_pickle=False)
+        for p, pid in enumerate(self.policy_ids):
+            self.ctx.params_set(p, z[f"{pid}/weights"])
+            b = z[f"{pid}/beta_powers"]
+            self.ctx.adam_set(p, z[f"{pid}/adam_m"], z[f"{pid}/adam_v"], float(b[0]), float(b[1]))
+            self.kl_coeff[p] = float(z[f"{pid}/kl_coeff"][0])
+        self.ctx.filter_set(float(z["filter/n"][0]), z["filter/M"], z["filter/S"])
+        meta = json.loads(bytes(z["meta"]).decode())
+        self.iteration, self.timesteps_total = meta["iteration"], meta["timesteps_total"]
+
+    def stop(self):
+        self.ctx.close()
+
+
+def update_kl(kl_coeff, sampled_kl, kl_target=0.01):
+    """RLlib PPO update_kl (ppo_tf_policy.KLCoeffMixin)."""
+    if sampled_kl > 2.0 * kl_target:
+        return kl_coeff * 1.5
+    if sampled_kl < 0.5 * kl_target:
+        return kl_coeff * 0.5
+    return kl_coeff
+
+
+def run(config, stop=None, n_envs=None, device=0, verbose=True):
+    """tune.run("PPO", config=config, stop={"timesteps_total": ...}) for one trial."""
+    stop = stop or {"training_iteration": 1}
+    tr = PPOTrainer(config, n_envs=n_envs, device=device)
+    results = []
+    while True:
+        r = tr.train()
+        results.append(r)
+        if verbose:
+            print(json.dumps({k: r[k] for k in ("training_iteration", "timesteps_total", "timers")}))
+        if any(r.get(k, 0) >= v for k, v in stop.items()):
+            break
+    tr.stop()
+    return results
