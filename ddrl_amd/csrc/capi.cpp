@@ -58,6 +58,9 @@ struct ddrl_ctx {
   float** stage_tab = nullptr;    // device array of per-policy stage pointers
   int32_t* zero_perm = nullptr;
   UpdateArgs* d_uargs = nullptr;  // device copy of the per-workgroup update arguments
+  unsigned long long* xchg = nullptr;  // norm^2 exchange granules of the update kernel
+  int* err = nullptr;                  // device error word (exchange timeout)
+  float kl_last[DDRL_MAXP] = {0};
   // host-variant staging
   float *h_obs = nullptr, *h_eps = nullptr, *h_act = nullptr;
   std::vector<void*> allocs;
@@ -179,7 +182,7 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
   rc = rc || dalloc(c, &c->f_n, 1) || dalloc(c, &c->f_M, DDRL_MAXFULL) || dalloc(c, &c->f_S, DDRL_MAXFULL) ||
        dalloc(c, &c->f_normc, 2 * DDRL_MAXFULL) || dalloc(c, &c->done_tn, (size_t)T * N) ||
        dalloc(c, &c->stage_tab, DDRL_MAXP) || dalloc(c, &c->zero_perm, 4) ||
-       dalloc(c, &c->d_uargs, DDRL_MAXP) ||
+       dalloc(c, &c->d_uargs, DDRL_MAXP) || dalloc(c, &c->xchg, 4 * DDRL_MAXP) || dalloc(c, &c->err, 1) ||
        dalloc(c, &c->h_obs, (size_t)N * g.obs_full_dim) ||
        dalloc(c, &c->h_eps, (size_t)N * g.n_agents * g.act_dim) || dalloc(c, &c->h_act, (size_t)N * 8);
   if (!rc) {
@@ -211,11 +214,21 @@ int ddrl_set_stream(ddrl_ctx* c, void* s) {
   return 0;
 }
 
+static int check_err(ddrl_ctx* c) {
+  int e = 0;
+  HIPCHK(hipMemcpy(&e, c->err, sizeof(int), hipMemcpyDeviceToHost));
+  if (e) {
+    (void)hipMemset(c->err, 0, sizeof(int));
+    return fail("update kernel: norm exchange between the policy and value workgroups timed out");
+  }
+  return 0;
+}
+
 int ddrl_synchronize(ddrl_ctx* c) {
   CHK_CTX(c);
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipGetLastError());
-  return 0;
+  return check_err(c);
 }
 
 int ddrl_param_count(ddrl_ctx* c, int pid, int64_t* n) {
@@ -432,6 +445,7 @@ int ddrl_ppo_update(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const 
     if (!(mask & (1 << p))) continue;
     if (!shuffle[p] || !perm[p]) return fail("null shuffle/perm for a masked policy");
     ua[n] = make_update(c, p, shuffle[p], perm[p], kl[p]);
+    c->kl_last[p] = kl[p];
     ua[n].max_steps = max_steps;
     const int total = c->cfg.num_sgd_iter * c->pol[p].nb;
     c->pol[p].last_steps = max_steps >= 0 ? std::min(total, max_steps) : total;
@@ -444,7 +458,8 @@ int ddrl_ppo_update(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const 
   // pageable source: the runtime stages (or blocks on) the copy before returning
   HIPCHK(hipMemcpyAsync(c->d_uargs, ua, sizeof(UpdateArgs) * n, hipMemcpyHostToDevice, c->stream));
   if (c->cfg.model_kind == DDRL_MODEL_FFN)
-    launch_update_ffn(c->stream, c->d_uargs, h, 128, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim, maxd);
+    launch_update_ffn(c->stream, c->d_uargs, h, 128, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim, maxd,
+                      c->xchg, c->err);
   else
     launch_update_gnn(c->stream, c->d_uargs, h, 128, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim);
   HIPCHK(hipGetLastError());
@@ -458,6 +473,15 @@ int ddrl_ppo_stats(ddrl_ctx* c, int pid, float* host, size_t n_steps) {
   if (n_steps > cap) return fail("more stats requested than the schedule holds");
   HIPCHK(hipMemcpyAsync(host, c->pol[pid].stats, n_steps * 8 * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  if (check_err(c)) return -1;
+  // the policy / value workgroups each write their own columns; total_loss is their
+  // linear combination: mean(-surr) + beta*mean(kl) + vf_coeff*mean(vf) - ent_coeff*mean(H)
+  const ddrl_cfg& g = c->cfg;
+  const float beta = c->kl_last[pid];
+  for (size_t k = 0; k < n_steps; ++k) {
+    float* s = host + 8 * k;
+    s[0] = s[1] + beta * s[3] + g.vf_loss_coeff * s[2] - g.entropy_coeff * s[4];
+  }
   return 0;
 }
 
@@ -472,7 +496,7 @@ int ddrl_ppo_grad(ddrl_ctx* c, int pid, const int32_t* rows, int n_rows, float k
   HIPCHK(hipMemcpyAsync(c->d_uargs, &u, sizeof(UpdateArgs), hipMemcpyHostToDevice, c->stream));
   if (c->cfg.model_kind == DDRL_MODEL_FFN)
     launch_update_ffn(c->stream, c->d_uargs, h, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim,
-                      c->pol[pid].d);
+                      c->pol[pid].d, c->xchg, c->err);
   else
     launch_update_gnn(c->stream, c->d_uargs, h, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim);
   HIPCHK(hipGetLastError());

@@ -50,6 +50,20 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// Sum over the 16 lanes of a DPP row (lanes 16q .. 16q+15, i.e. over c for fixed q), every
+// lane of the row receives the total.  Fixed order: xor 1, xor 2, half-mirror, mirror.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);  // row_half_mirror
+  v += dpp_mov<0x140>(v);  // row_mirror
+  return v;
+}
+
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -87,44 +101,51 @@ __device__ __forceinline__ int wbase(int r) {
   return c * 64 + ((4 * q + r) ^ swz(c));
 }
 
-// Forward of one branch for the 16 rows of this wave.
-//   xop[s] : B operand of layer 1 at k-step s, i.e. X[row = c][f = 4s + q] (0 beyond d)
-//   KS1    : k-steps of layer 1 (ceil(d / 4)); W1 rows beyond d are zero in LDS
-// Outputs h1[4], h2[4] (transposed activation tiles), out[O] (identical in the 4 q-lanes).
-template <int O, int KS1>
-__device__ __forceinline__ void ffn_branch_fwd(const NetLds& W, const float* xop,
-                                               floatx4 h1[4], floatx4 h2[4], float out[O]) {
-  const int lane = threadIdx.x & 63, q = lane >> 4;
+// Forward of one branch for RT row tiles (16 rows each) of this wave.
+//   xop[t][s] : B operand of layer 1 at k-step s for row tile t, X[row = c][f = 4s + q]
+//   KS1       : k-steps of layer 1 (ceil(d / 4)); W1 rows beyond d are zero in LDS
+// Outputs h1[t][4], h2[t][4] (transposed activation tiles), out[t][O] (same in the 4 q-lanes).
+// Every weight operand read from LDS feeds RT MFMAs.
+template <int O, int KS1, int RT>
+__device__ __forceinline__ void ffn_fwd_rt(const NetLds& W, const float (*xop)[12],
+                                           floatx4 (*h1)[4], floatx4 (*h2)[4], float (*out)[O]) {
+  const int lane = threadIdx.x & 63, q = lane >> 4, c = lane & 15;
 #pragma unroll
   for (int ob = 0; ob < 4; ++ob) {
     const int o0 = 16 * ob + 4 * q;
     floatx4 b = {W.b1[o0], W.b1[o0 + 1], W.b1[o0 + 2], W.b1[o0 + 3]};
-    h1[ob] = b;
+#pragma unroll
+    for (int t = 0; t < RT; ++t) h1[t][ob] = b;
   }
   {
     const int rb[4] = {rbase(0), rbase(1), rbase(2), rbase(3)};
 #pragma unroll
     for (int s = 0; s < KS1; ++s) {
       const float* wp = W.w1 + rb[s & 3] + 1024 * (s >> 2);
-      const float bx = xop[s];
 #pragma unroll
-      for (int ob = 0; ob < 4; ++ob) h1[ob] = mfma4(wp[16 * ob], bx, h1[ob]);
+      for (int ob = 0; ob < 4; ++ob) {
+        const float a = wp[16 * ob];
+#pragma unroll
+        for (int t = 0; t < RT; ++t) h1[t][ob] = mfma4(a, xop[t][s], h1[t][ob]);
+      }
     }
   }
 #pragma unroll
-  for (int ob = 0; ob < 4; ++ob)
+  for (int t = 0; t < RT; ++t)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) h1[ob][r] = tanhf(h1[ob][r]);
+    for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h1[t][ob][r] = tanhf(h1[t][ob][r]);
 
 #pragma unroll
   for (int ob = 0; ob < 4; ++ob) {
     const int o0 = 16 * ob + 4 * q;
     floatx4 b = {W.b2[o0], W.b2[o0 + 1], W.b2[o0 + 2], W.b2[o0 + 3]};
-    h2[ob] = b;
+#pragma unroll
+    for (int t = 0; t < RT; ++t) h2[t][ob] = b;
   }
   {
     // row f = 16fb + 4q + r  ->  same swizzle as rbase with (4q + r) as the row
-    const int c = lane & 15;
     int fb_base[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -136,26 +157,47 @@ __device__ __forceinline__ void ffn_branch_fwd(const NetLds& W, const float* xop
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float* wp = W.w2 + fb_base[r] + 1024 * fb;
-        const float bx = h1[fb][r];
 #pragma unroll
-        for (int ob = 0; ob < 4; ++ob) h2[ob] = mfma4(wp[16 * ob], bx, h2[ob]);
+        for (int ob = 0; ob < 4; ++ob) {
+          const float a = wp[16 * ob];
+#pragma unroll
+          for (int t = 0; t < RT; ++t) h2[t][ob] = mfma4(a, h1[t][fb][r], h2[t][ob]);
+        }
       }
   }
 #pragma unroll
-  for (int ob = 0; ob < 4; ++ob)
+  for (int t = 0; t < RT; ++t)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) h2[ob][r] = tanhf(h2[ob][r]);
+    for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h2[t][ob][r] = tanhf(h2[t][ob][r]);
 
   // Linear head: partial dot over this lane's 16 features, then sum over q.
 #pragma unroll
   for (int o = 0; o < O; ++o) {
-    float acc = 0.f;
+    float acc[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) acc[t] = 0.f;
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc = fmaf(h2[fb][r], W.wo[(16 * fb + 4 * q + r) * O + o], acc);
-    out[o] = qsum(acc) + W.bo[o];
+      for (int r = 0; r < 4; ++r) {
+        const float wv = W.wo[(16 * fb + 4 * q + r) * O + o];
+#pragma unroll
+        for (int t = 0; t < RT; ++t) acc[t] = fmaf(h2[t][fb][r], wv, acc[t]);
+      }
+#pragma unroll
+    for (int t = 0; t < RT; ++t) out[t][o] = qsum(acc[t]) + W.bo[o];
   }
+}
+
+// Single-tile form used by the rollout forward.
+template <int O, int KS1>
+__device__ __forceinline__ void ffn_branch_fwd(const NetLds& W, const float* xop,
+                                               floatx4 h1[4], floatx4 h2[4], float out[O]) {
+  ffn_fwd_rt<O, KS1, 1>(W, reinterpret_cast<const float (*)[12]>(xop),
+                        reinterpret_cast<floatx4 (*)[4]>(h1), reinterpret_cast<floatx4 (*)[4]>(h2),
+                        reinterpret_cast<float (*)[O]>(out));
 }
 
 // tanh derivative applied in place: d = d * (1 - h^2)
@@ -183,19 +225,28 @@ __device__ __forceinline__ void head_bwd(const NetLds& W, const float* dout, flo
 }
 
 // dH1^T = W2 . dZ2^T   (MFMA, A = W2[f = 16fb + c][o = 16ob + 4q + r], B = dZ2 tile regs)
-__device__ __forceinline__ void layer2_bwd(const NetLds& W, const floatx4 dz2[4], floatx4 dh1[4]) {
+template <int RT>
+__device__ __forceinline__ void layer2_bwd_rt(const NetLds& W, const floatx4 (*dz2)[4], floatx4 (*dh1)[4]) {
 #pragma unroll
-  for (int fb = 0; fb < 4; ++fb) dh1[fb] = splat4(0.f);
+  for (int t = 0; t < RT; ++t)
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb) dh1[t][fb] = splat4(0.f);
   const int wb[4] = {wbase(0), wbase(1), wbase(2), wbase(3)};
 #pragma unroll 2
   for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float bx = dz2[ob][r];
       const float* wp = W.w2 + wb[r] + 16 * ob;
 #pragma unroll
-      for (int fb = 0; fb < 4; ++fb) dh1[fb] = mfma4(wp[1024 * fb], bx, dh1[fb]);
+      for (int fb = 0; fb < 4; ++fb) {
+        const float a = wp[1024 * fb];
+#pragma unroll
+        for (int t = 0; t < RT; ++t) dh1[t][fb] = mfma4(a, dz2[t][ob][r], dh1[t][fb]);
+      }
     }
+}
+__device__ __forceinline__ void layer2_bwd(const NetLds& W, const floatx4 dz2[4], floatx4 dh1[4]) {
+  layer2_bwd_rt<1>(W, reinterpret_cast<const floatx4 (*)[4]>(dz2), reinterpret_cast<floatx4 (*)[4]>(dh1));
 }
 
 // Write a transposed activation tile set (rows 16*tile + c, features 16fb+4q+r) into an
@@ -223,6 +274,27 @@ __device__ __forceinline__ floatx4 dw_tile(const float* A, const float* B, int f
     for (int v = 0; v < 4; ++v) acc = mfma4(ap[rb[v] + 1024 * u], bp[rb[v] + 1024 * u], acc);
   }
   return acc;
+}
+
+// Two independent 16x16 dW tiles in one pass (two accumulation chains interleaved, so a
+// single wave per SIMD keeps the MFMA pipe busy despite the 40-cycle dependent latency).
+template <int NROWS>
+__device__ __forceinline__ void dw_tile2(const float* A, const float* B, int fa0, int fo0, int fa1, int fo1,
+                                         floatx4& t0, floatx4& t1) {
+  floatx4 a0 = splat4(0.f), a1 = splat4(0.f);
+  const int rb[4] = {rbase(0), rbase(1), rbase(2), rbase(3)};
+  const float *ap0 = A + 16 * fa0, *bp0 = B + 16 * fo0, *ap1 = A + 16 * fa1, *bp1 = B + 16 * fo1;
+#pragma unroll 2
+  for (int u = 0; u < NROWS / 16; ++u) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int o = rb[v] + 1024 * u;
+      a0 = mfma4(ap0[o], bp0[o], a0);
+      a1 = mfma4(ap1[o], bp1[o], a1);
+    }
+  }
+  t0 = a0;
+  t1 = a1;
 }
 
 // Same with B given as a plain [rows][O] (O <= 16) row-major array, zero beyond O.

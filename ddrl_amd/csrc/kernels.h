@@ -103,7 +103,8 @@ struct UpdateHyper {
   int P;
 };
 // ua_dev: device array of h.P UpdateArgs (one persistent workgroup per entry)
-void launch_update_ffn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHyper& h, int nrows, float inv_n, int A, int d);
+void launch_update_ffn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHyper& h, int nrows, float inv_n, int A, int d,
+                       unsigned long long* xchg, int* err);
 void launch_update_gnn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHyper& h, int nrows, float inv_n, int A);
 // clip_by_global_norm + tf1 Adam on a flat (all-reduced) gradient vector
 void launch_apply_adam(hipStream_t s, const float* grad, int n, float* theta, float* m, float* v,

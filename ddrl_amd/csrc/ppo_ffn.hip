@@ -1,385 +1,545 @@
-// a13-a17: fused PPO minibatch SGD for the fcnet policy/value model.
+// a13-a17: fused PPO minibatch SGD for the fcnet policy/value model (persistent kernel).
 //
-// One persistent workgroup (8 waves, 512 threads) per policy runs the policy's whole
-// minibatch schedule -- num_sgd_iter epochs x nb minibatches of 128 rows -- without
-// returning to the host.  Per minibatch step:
-//   gather 128 rows (row = shuffle[perm[e][b] * 128 + i], RLlib TrainTFMultiGPU slicing)
-//   -> forward of the policy branch (MFMA, activations in registers, 16 rows per wave)
-//   -> PPOLoss per row and analytic dL/dlogits (DiagGaussian logp / KL / entropy, clipped
-//      surrogate; RLlib 1.0 ppo_tf_policy.PPOLoss)
-//   -> backward (head VALU, layer 2 MFMA from registers), activations to LDS, weight
-//      gradients as 16x16 MFMA tiles over the 128 rows (K = rows), bias column sums
-//   -> the same for the value branch (PPO2 clipped value loss, vf_clip_param)
-//   -> global-norm clip (tf.clip_by_global_norm(grads, 0.5)) via a workgroup reduction
-//   -> tf1 Adam (ApplyAdam) on every parameter; weights updated in place in LDS,
-//      m / v in HBM (L2 resident), beta powers as fp32 like the TF variables.
-// Gradients never leave the registers of the wave that produced them.
+// Two workgroups per policy, on two CUs: blockIdx = 2p + branch, branch 0 = policy branch
+// (fc_1, fc_2, fc_out), branch 1 = value branch (fc_value_1, fc_value_2, value_out).  The
+// branches share no parameters, so each workgroup computes its own gradients and runs Adam
+// on its own parameters; the only coupling is tf.clip_by_global_norm, which needs the
+// squared norm over ALL variables: every step the two workgroups swap their partial
+// squared norms through one tagged 8-byte granule each (sc1 store / sc1 poll, slots double
+// buffered by step parity, zeroed by a memset before every launch, spins bounded).
+//
+// Per minibatch step (RLlib TrainTFMultiGPU: row = shuffle[perm[e][b] * 128 + i]):
+//   rows of step s+1 are prefetched into registers while step s computes;
+//   forward of the branch for 32 rows per wave, one wave per SIMD (MFMA 16x16x4 f32,
+//   activations in registers, every weight operand read from LDS feeds two MFMAs);
+//   PPOLoss per row (RLlib 1.0 ppo_tf_policy.PPOLoss) and analytic dL/d(outputs);
+//   head / bias gradients and loss statistics by DPP row reductions (no LDS round trip);
+//   layer-2 backward from registers; H1/dZ2 then X/dZ1 through LDS for the two weight-
+//   gradient GEMMs (16x16 tiles, K = 128 rows); per-wave tile ownership;
+//   global-norm clip; tf1 Adam (ApplyAdam) with m / v held in registers by the owning
+//   lane and the weights updated in place in the LDS image.
 #include "common.h"
 #include "kernels.h"
 #include "ffn.h"
 
+#define NT 256   // 4 waves: one per SIMD, 32 rows (two 16-row tiles) each
+#define NW 4
+
 struct UpdateBatch {
-  const UpdateArgs* a;   // device array, one entry per workgroup (policy)
+  const UpdateArgs* a;   // device array, one entry per policy
   UpdateHyper h;
-  int nrows;      // rows per minibatch handled here (<= 128)
-  float inv_n;    // 1 / sgd_minibatch_size (global minibatch)
+  int nrows;             // rows per minibatch handled here (<= 128)
+  float inv_n;           // 1 / sgd_minibatch_size (global minibatch)
+  unsigned long long* xchg;  // [P][2 branches][2 parities] tagged norm^2 granules
+  int* err;              // set to 1 if a norm exchange timed out
 };
 
-#define NT 512
-#define NW 8
-#define SCR_ROWS 128
+// Per-branch view of the flat (Keras-order) parameter vector.
+struct BranchOff { int w1, b1, w2, b2, wo, bo; };
+__device__ __forceinline__ BranchOff branch_off(const FfnOffsets& o, bool pol) {
+  BranchOff b;
+  b.w1 = pol ? o.w1 : o.vw1; b.b1 = pol ? o.b1 : o.vb1;
+  b.w2 = pol ? o.w2 : o.vw2; b.b2 = pol ? o.b2 : o.vb2;
+  b.wo = pol ? o.wo : o.vo;  b.bo = pol ? o.bo : o.vbo;
+  return b;
+}
 
-// Store a 16x16 gradient tile (C layout: dW[f = 16fa + 4q + r][o = 16fo + c]) of a
-// row-major [rows][ncols] parameter block at global offset `off`; returns its sum of squares.
-__device__ __forceinline__ float store_grad_tile(float* G, int off, int ncols, int nrows_valid,
-                                                 int fa, int fo, const floatx4& t) {
-  const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
-  const int o = 16 * fo + c;
-  float ss = 0.f;
-  if (o < ncols) {
+template <int OB>
+__device__ void stage_branch(const float* __restrict__ th, int d, const BranchOff& bo, float* lds,
+                             NetLds& W) {
+  W.w1 = lds; W.w2 = W.w1 + 48 * 64; W.b1 = W.w2 + 64 * 64; W.b2 = W.b1 + 64;
+  W.wo = W.b2 + 64; W.bo = W.wo + 64 * OB;
+  for (int i = threadIdx.x; i < 48 * 64; i += NT) {
+    const int f = i >> 6;
+    W.w1[sidx(f, i & 63)] = f < d ? th[bo.w1 + i] : 0.f;
+  }
+  for (int i = threadIdx.x; i < 64 * 64; i += NT) W.w2[sidx(i >> 6, i & 63)] = th[bo.w2 + i];
+  for (int i = threadIdx.x; i < 64; i += NT) { W.b1[i] = th[bo.b1 + i]; W.b2[i] = th[bo.b2 + i]; }
+  for (int i = threadIdx.x; i < 64 * OB; i += NT) W.wo[i] = th[bo.wo + i];
+  for (int i = threadIdx.x; i < OB; i += NT) W.bo[i] = th[bo.bo + i];
+}
+#define BRANCH_LDS_FLOATS (48 * 64 + 64 * 64 + 128 + 64 * 16 + 16)
+
+// "Small" parameters owned one per thread: [dWo 64*OB][dbo OB][db1 64][db2 64]
+template <int OB>
+__device__ __forceinline__ void small_param(int e, const BranchOff& bo, const NetLds& W, int& pidx, float*& lp) {
+  if (e < 64 * OB) { pidx = bo.wo + e; lp = W.wo + e; return; }
+  e -= 64 * OB;
+  if (e < OB) { pidx = bo.bo + e; lp = W.bo + e; return; }
+  e -= OB;
+  if (e < 64) { pidx = bo.b1 + e; lp = W.b1 + e; return; }
+  e -= 64;
+  pidx = bo.b2 + e; lp = W.b2 + e;
+}
+
+template <int A>
+struct RowData {
+  float x[2][12];      // two row tiles
+  float act[2][A];
+  float ol[2][2 * A];
+  float s0[2], s1[2];  // policy: logp_old, adv;  value: vf_old, vt
+};
+
+template <int A, int KS1, bool POL>
+__device__ __forceinline__ void load_row(const UpdateArgs& U, const int* ridx, const bool* ok, RowData<A>& r) {
+  const int q = (threadIdx.x & 63) >> 4;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int f = 16 * fa + 4 * q + r;
-      if (f < nrows_valid) {
-        G[off + f * ncols + o] = t[r];
-        ss += t[r] * t[r];
-      }
+  for (int t = 0; t < 2; ++t) {
+    const float* rp = U.rec + (size_t)ridx[t] * U.lay.stride;
+#pragma unroll
+    for (int s = 0; s < 12; ++s) {
+      const int f = 4 * s + q;
+      r.x[t][s] = (ok[t] && s < KS1 && f < U.d) ? rp[U.lay.obs + f] : 0.f;
+    }
+    if (POL) {
+#pragma unroll
+      for (int j = 0; j < A; ++j) r.act[t][j] = rp[U.lay.act + j];
+#pragma unroll
+      for (int j = 0; j < 2 * A; ++j) r.ol[t][j] = rp[U.lay.logit + j];
+      r.s0[t] = rp[U.lay.logp];
+      r.s1[t] = rp[U.lay.adv];
+    } else {
+#pragma unroll
+      for (int j = 0; j < A; ++j) r.act[t][j] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 2 * A; ++j) r.ol[t][j] = 0.f;
+      r.s0[t] = rp[U.lay.vf];
+      r.s1[t] = rp[U.lay.vt];
     }
   }
-  return ss;
 }
 
-// LDS location of parameter `i` (Keras flat order) inside the two-branch weight image.
-template <int O>
-__device__ __forceinline__ float* param_lds(int i, const FfnOffsets& of, const NetLds& P, const NetLds& V) {
-  if (i < of.b1) return P.w1 + sidx(i >> 6, i & 63);
-  if (i < of.vw1) return P.b1 + (i - of.b1);
-  if (i < of.vb1) { const int j = i - of.vw1; return V.w1 + sidx(j >> 6, j & 63); }
-  if (i < of.w2) return V.b1 + (i - of.vb1);
-  if (i < of.b2) { const int j = i - of.w2; return P.w2 + sidx(j >> 6, j & 63); }
-  if (i < of.vw2) return P.b2 + (i - of.b2);
-  if (i < of.vb2) { const int j = i - of.vw2; return V.w2 + sidx(j >> 6, j & 63); }
-  if (i < of.wo) return V.b2 + (i - of.vb2);
-  if (i < of.bo) return P.wo + (i - of.wo);
-  if (i < of.vo) return P.bo + (i - of.bo);
-  if (i < of.vbo) return V.wo + (i - of.vo);
-  return V.bo;
+__device__ __forceinline__ int row_index(const UpdateArgs& U, int step, int row_l, bool ok) {
+  if (!ok) return 0;
+  const int e = step / U.nb, b = step - e * U.nb;
+  return U.shuffle[U.perm[e * U.nb + b] * DDRL_MB + row_l];
 }
 
-__device__ __forceinline__ void tile_coords(int t, int& type, int& fa, int& fo) {
-  if (t < 4) { type = 0; fa = t; fo = 0; }
-  else if (t < 20) { type = 1; fa = (t - 4) >> 2; fo = (t - 4) & 3; }
-  else { type = 2; fa = (t - 20) >> 2; fo = (t - 20) & 3; }
+// Per-row PPO loss terms and output gradient (policy branch).
+template <int A>
+__device__ __forceinline__ void policy_loss_row(const float* out, const float* act, const float* ol,
+                                                float logp_old, float adv, float beta, float lo, float hi,
+                                                float ent_coeff, float inv_n, bool ok, float* dout, float* st) {
+  float logp = -0.5f * (float)(DDRL_LOG2PI * A), klr = 0.f, ent = 0.f;
+  float z[A], sd[A];
+#pragma unroll
+  for (int j = 0; j < A; ++j) {
+    sd[j] = expf(out[A + j]);
+    z[j] = (act[j] - out[j]) / sd[j];
+    logp -= 0.5f * z[j] * z[j];
+    logp -= out[A + j];
+    const float v0 = expf(ol[A + j]);
+    const float dm = ol[j] - out[j];
+    klr += out[A + j] - ol[A + j] + (v0 * v0 + dm * dm) / (2.f * sd[j] * sd[j]) - 0.5f;
+    ent += out[A + j] + 0.5f * (float)(DDRL_LOG2PI + 1.0);
+  }
+  const float ratio = expf(logp - logp_old);
+  const float cr = fminf(fmaxf(ratio, lo), hi);
+  const float s1 = adv * ratio, s2 = adv * cr;
+  const float surr = fminf(s1, s2);
+  const float dr = (s1 <= s2) ? adv : ((ratio >= lo && ratio <= hi) ? adv : 0.f);
+  const float glogp = -dr * ratio;
+#pragma unroll
+  for (int j = 0; j < A; ++j) {
+    const float v0 = expf(ol[A + j]);
+    const float dm = ol[j] - out[j];
+    const float var1 = sd[j] * sd[j];
+    const float dmu = glogp * (z[j] / sd[j]) + beta * ((out[j] - ol[j]) / var1);
+    const float dls = glogp * (z[j] * z[j] - 1.f) + beta * (1.f - (v0 * v0 + dm * dm) / var1) - ent_coeff;
+    dout[j] = ok ? dmu * inv_n : 0.f;
+    dout[A + j] = ok ? dls * inv_n : 0.f;
+  }
+  st[0] = ok ? -surr : 0.f;
+  st[1] = ok ? klr : 0.f;
+  st[2] = ok ? ent : 0.f;
 }
 
-template <int A, int KS1>
-__global__ void __launch_bounds__(NT) k_update_ffn(UpdateBatch ub) {
-  constexpr int O = 2 * A;
-  extern __shared__ float lds[];
-  const int p = blockIdx.x;
-  const UpdateArgs U = ub.a[p];
+// Per-row clipped value loss (RLlib 1.0 PPO2 style, or later RLlib's clip of the square).
+__device__ __forceinline__ void value_loss_row(float V, float vfo, float vtg, const UpdateHyper& H,
+                                               float inv_n, bool ok, float* dout, float* st) {
+  float vf, dvf;
+  if (H.vf_mode == 0) {
+    const float vf1 = (V - vtg) * (V - vtg);
+    const float dv = V - vfo;
+    const float vcl = vfo + fminf(fmaxf(dv, -H.vf_clip), H.vf_clip);
+    const float vf2 = (vcl - vtg) * (vcl - vtg);
+    vf = fmaxf(vf1, vf2);
+    dvf = (vf1 >= vf2) ? 2.f * (V - vtg)
+                       : ((dv >= -H.vf_clip && dv <= H.vf_clip) ? 2.f * (vcl - vtg) : 0.f);
+  } else {
+    const float sq = (V - vtg) * (V - vtg);
+    vf = fminf(sq, H.vf_clip);
+    dvf = sq <= H.vf_clip ? 2.f * (V - vtg) : 0.f;
+  }
+  dout[0] = ok ? H.vf_coeff * dvf * inv_n : 0.f;
+  const float dd = vtg - V;
+  st[0] = ok ? vf : 0.f;
+  st[1] = ok ? vtg : 0.f;
+  st[2] = ok ? vtg * vtg : 0.f;
+  st[3] = ok ? dd : 0.f;
+  st[4] = ok ? dd * dd : 0.f;
+}
+
+#define NS1 4   // dW2 tile slots per wave (16 tiles / 4 waves)
+#define NS2 3   // dW1 tile slots per wave (<= 12 tiles / 4 waves)
+
+template <int A, int KS1, int OB, bool POL>
+__device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBatch& ub, float* lds, int p) {
   const UpdateHyper& H = ub.h;
   const int d = U.d;
   const FfnOffsets of = ffn_offsets(d, A);
+  const BranchOff bo = branch_off(of, POL);
   const int nf1 = (d + 15) >> 4;
-  const int T_net = 20 + 4 * nf1;
+  constexpr int NSB = 64 * OB + OB + 128;          // small params of this branch
+  constexpr int NSLOT = (NSB + NT - 1) / NT;
+  constexpr int NSTAT = POL ? 3 : 5;
+  constexpr int NTS = NS1 + NS2;
 
-  NetLds PW, VW;
-  stage_weights(U.theta, d, A, lds, PW, VW, NT);
-  float* bufA = lds + LDS_WEIGHTS_FLOATS(O);
+  NetLds W;
+  stage_branch<OB>(U.theta, d, bo, lds, W);
+  float* bufA = lds + BRANCH_LDS_FLOATS;
   float* bufB = bufA + 128 * 64;
-  float* D = bufB + 128 * 64;             // [128][O]
-  float* scr = D + 128 * 16;              // [8][128] per-row stats
-  float* red = scr + 8 * SCR_ROWS;        // [32]
-  __syncthreads();
+  float* Pb = bufB + 128 * 64;              // [NW][NSB] per-wave partial small grads
+  float* red = Pb + NW * NSB;               // [NW][8] row-stat partials, [64..] scalars
 
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, q = lane >> 4, w = tid >> 6;
-  const int row_l = 16 * w + c;            // row of this lane inside the minibatch
-  const bool row_ok = row_l < ub.nrows;
+  int row_l[2];
+  bool row_ok[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    row_l[t] = 32 * w + 16 * t + c;
+    row_ok[t] = row_l[t] < ub.nrows;
+  }
+
+  // ---- optimizer state of the parameters this lane owns ----
+  // slots 0..3: dW2 tiles w, w+4, w+8, w+12;  slots 4..6: dW1 tiles w, w+4, w+8 (if < 4*nf1)
+  floatx4 mt[NTS], vt4[NTS];
+  bool tv[NTS];
+  int tfa[NTS], tfo[NTS];
+#pragma unroll
+  for (int i = 0; i < NTS; ++i) {
+    const int tt = i < NS1 ? w + 4 * i : w + 4 * (i - NS1);
+    tv[i] = i < NS1 ? true : (tt < 4 * nf1);
+    tfa[i] = tt >> 2;
+    tfo[i] = tt & 3;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = 16 * tfa[i] + 4 * q + r, o = 16 * tfo[i] + c;
+      const bool ok = tv[i] && (i < NS1 || f < d);
+      const int pidx = (i < NS1 ? bo.w2 : bo.w1) + f * 64 + o;
+      mt[i][r] = ok ? U.m[pidx] : 0.f;
+      vt4[i][r] = ok ? U.v[pidx] : 0.f;
+    }
+  }
+  float ms[NSLOT], vs[NSLOT];
+#pragma unroll
+  for (int k = 0; k < NSLOT; ++k) {
+    const int e = tid + NT * k;
+    ms[k] = vs[k] = 0.f;
+    if (e < NSB) {
+      int pidx; float* lp;
+      small_param<OB>(e, bo, W, pidx, lp);
+      ms[k] = U.m[pidx];
+      vs[k] = U.v[pidx];
+    }
+  }
   float b1p = U.beta_pow[0], b2p = U.beta_pow[1];
   const float adv_mean = U.adv_norm[0], adv_den = U.adv_norm[1];
   const float beta = U.kl_coeff;
   const float lo = 1.f - H.clip, hi = 1.f + H.clip;
+  __syncthreads();
 
   const int total_steps = U.n_epochs * U.nb;
   const int last = U.max_steps >= 0 ? min(total_steps, U.step0 + U.max_steps) : total_steps;
+  RowData<A> cur;
+  int idx_nxt[2] = {0, 0};
+  if (U.step0 < last) {
+    int ix[2] = {row_index(U, U.step0, row_l[0], row_ok[0]), row_index(U, U.step0, row_l[1], row_ok[1])};
+    load_row<A, KS1, POL>(U, ix, row_ok, cur);
+  }
+  if (U.step0 + 1 < last) {
+    idx_nxt[0] = row_index(U, U.step0 + 1, row_l[0], row_ok[0]);
+    idx_nxt[1] = row_index(U, U.step0 + 1, row_l[1], row_ok[1]);
+  }
+
   for (int step = U.step0; step < last; ++step) {
-    const int e = step / U.nb, b = step - e * U.nb;
-    int ridx = 0;
-    if (row_ok) ridx = U.shuffle[U.perm[e * U.nb + b] * DDRL_MB + row_l];
-    const float* rp = U.rec + (size_t)ridx * U.lay.stride;
-    float xop[12];
-#pragma unroll
-    for (int s = 0; s < 12; ++s) {
-      const int f = 4 * s + q;
-      xop[s] = (row_ok && s < KS1 && f < d) ? rp[U.lay.obs + f] : 0.f;
-    }
-    float act[A], olog[O];
-#pragma unroll
-    for (int j = 0; j < A; ++j) act[j] = rp[U.lay.act + j];
-#pragma unroll
-    for (int j = 0; j < O; ++j) olog[j] = rp[U.lay.logit + j];
-    const float ologp = rp[U.lay.logp];
-    const float vf_old = rp[U.lay.vf];
-    const float adv = (rp[U.lay.adv] - adv_mean) / adv_den;
-    const float vt = rp[U.lay.vt];
 
-    // gradients go straight to G (L2-resident) as each tile / column sum completes
-    float* G = U.grad_out ? U.grad_out : U.gscr;
-    float ss = 0.f;   // this thread's share of the squared global norm
-
-#pragma unroll
-    for (int net = 0; net < 2; ++net) {
-      const NetLds& W = net == 0 ? PW : VW;
-      floatx4 h1[4], h2[4], dz2[4], dz1[4];
-      float dout[O];
-      if (net == 0) {
-        float logits[O];
-        ffn_branch_fwd<O, KS1>(W, xop, h1, h2, logits);
-        // ---- PPOLoss (per row) and dL/dlogits ----
-        float logp = -0.5f * (float)(DDRL_LOG2PI * A), klr = 0.f, ent = 0.f;
-        float z[A], sd[A];
-#pragma unroll
-        for (int j = 0; j < A; ++j) {
-          sd[j] = expf(logits[A + j]);
-          z[j] = (act[j] - logits[j]) / sd[j];
-          logp -= 0.5f * z[j] * z[j];
-          logp -= logits[A + j];
-          const float v0 = expf(olog[A + j]);
-          const float dm = olog[j] - logits[j];
-          klr += logits[A + j] - olog[A + j] + (v0 * v0 + dm * dm) / (2.f * sd[j] * sd[j]) - 0.5f;
-          ent += logits[A + j] + 0.5f * (float)(DDRL_LOG2PI + 1.0);
-        }
-        const float ratio = expf(logp - ologp);
-        const float cr = fminf(fmaxf(ratio, lo), hi);
-        const float s1 = adv * ratio, s2 = adv * cr;
-        const float surr = fminf(s1, s2);
-        const float dr = (s1 <= s2) ? adv : ((ratio >= lo && ratio <= hi) ? adv : 0.f);
-        const float glogp = -dr * ratio;
-#pragma unroll
-        for (int j = 0; j < A; ++j) {
-          const float v0 = expf(olog[A + j]);
-          const float dm = olog[j] - logits[j];
-          const float var1 = sd[j] * sd[j];
-          float dmu = glogp * (z[j] / sd[j]) + beta * ((logits[j] - olog[j]) / var1);
-          float dls = glogp * (z[j] * z[j] - 1.f) + beta * (1.f - (v0 * v0 + dm * dm) / var1) - H.ent_coeff;
-          dout[j] = row_ok ? dmu * ub.inv_n : 0.f;
-          dout[A + j] = row_ok ? dls * ub.inv_n : 0.f;
-        }
-        if (q == 0 && row_ok) {
-          scr[0 * SCR_ROWS + row_l] = -surr;
-          scr[1 * SCR_ROWS + row_l] = klr;
-          scr[2 * SCR_ROWS + row_l] = ent;
-        }
+    // ---- forward + loss + output gradient (two row tiles) ----
+    floatx4 h1[2][4], h2[2][4], dz[2][4];
+    float out[2][OB], dout[2][OB];
+    ffn_fwd_rt<OB, KS1, 2>(W, cur.x, h1, h2, out);
+    float st[NSTAT];
+    {
+      float st0[NSTAT], st1[NSTAT];
+      if constexpr (POL) {
+        policy_loss_row<A>(out[0], cur.act[0], cur.ol[0], cur.s0[0], (cur.s1[0] - adv_mean) / adv_den,
+                           beta, lo, hi, H.ent_coeff, ub.inv_n, row_ok[0], dout[0], st0);
+        policy_loss_row<A>(out[1], cur.act[1], cur.ol[1], cur.s0[1], (cur.s1[1] - adv_mean) / adv_den,
+                           beta, lo, hi, H.ent_coeff, ub.inv_n, row_ok[1], dout[1], st1);
       } else {
-        float vo[1];
-        ffn_branch_fwd<1, KS1>(W, xop, h1, h2, vo);
-        const float V = vo[0];
-        float vf, dvf;
-        if (H.vf_mode == 0) {
-          const float vf1 = (V - vt) * (V - vt);
-          const float dv = V - vf_old;
-          const float vcl = vf_old + fminf(fmaxf(dv, -H.vf_clip), H.vf_clip);
-          const float vf2 = (vcl - vt) * (vcl - vt);
-          vf = fmaxf(vf1, vf2);
-          dvf = (vf1 >= vf2) ? 2.f * (V - vt)
-                             : ((dv >= -H.vf_clip && dv <= H.vf_clip) ? 2.f * (vcl - vt) : 0.f);
-        } else {
-          const float sq = (V - vt) * (V - vt);
-          vf = fminf(sq, H.vf_clip);
-          dvf = sq <= H.vf_clip ? 2.f * (V - vt) : 0.f;
-        }
-        dout[0] = row_ok ? H.vf_coeff * dvf * ub.inv_n : 0.f;
-        if (q == 0 && row_ok) {
-          scr[3 * SCR_ROWS + row_l] = vf;
-          scr[4 * SCR_ROWS + row_l] = V;
-          scr[5 * SCR_ROWS + row_l] = vt;
-        }
+        value_loss_row(out[0][0], cur.s0[0], cur.s1[0], H, ub.inv_n, row_ok[0], dout[0], st0);
+        value_loss_row(out[1][0], cur.s0[1], cur.s1[1], H, ub.inv_n, row_ok[1], dout[1], st1);
       }
-      constexpr int OMAX = O;
-      const int OO = net == 0 ? O : 1;
-      // ---- backward through the head (registers), then publish H2 / dZ2 / dout ----
-      if (net == 0) head_bwd<O>(W, dout, dz2);
-      else head_bwd<1>(W, dout, dz2);
-      dtanh_inplace(dz2, h2);
-      __syncthreads();                       // previous phase readers of bufA/bufB/D done
-      store_act(bufA, w, h2);
-      store_act(bufB, w, dz2);
-      if (q == 0) {
 #pragma unroll
-        for (int o = 0; o < OMAX; ++o)
-          if (o < OO) D[row_l * OO + o] = dout[o];
-      }
-      layer2_bwd(W, dz2, dz1);
-      dtanh_inplace(dz1, h1);
-      __syncthreads();
-      // ---- phase 0: dWo tiles (H2 x dout), db2, dbo ----
-      const int boff = net == 0 ? 0 : 128;
-#pragma unroll 1
-      for (int i = 0; i < 4; ++i) {
-        const int t = w + 8 * i;
-        if (t < 4) {
-          if (net == 0) ss += store_grad_tile(G, of.wo, O, 64, t, 0, dw_tile_head<O, DDRL_MB>(bufA, D, t));
-          else ss += store_grad_tile(G, of.vo, 1, 64, t, 0, dw_tile_head<1, DDRL_MB>(bufA, D, t));
-        }
-      }
-      if (tid >= boff && tid < boff + 64) {
-        float s = 0.f;
-        for (int r = 0; r < DDRL_MB; ++r) s += bufB[sidx(r, tid - boff)];
-        G[(net ? of.vb2 : of.b2) + tid - boff] = s;   // db2
-        ss += s * s;
-      } else if (tid >= boff + 64 && tid < boff + 64 + OO) {
-        float s = 0.f;
-        for (int r = 0; r < DDRL_MB; ++r) s += D[r * OO + (tid - boff - 64)];
-        G[(net ? of.vbo : of.bo) + tid - boff - 64] = s;   // dbo
-        ss += s * s;
-      }
-      __syncthreads();
-      // ---- phase 1: H1 -> A ; dW2 tiles (H1 x dZ2) ----
-      store_act(bufA, w, h1);
-      __syncthreads();
-#pragma unroll 1
-      for (int i = 0; i < 4; ++i) {
-        const int t = w + 8 * i;
-        if (t >= 4 && t < 20) {
-          int type, fa, fo;
-          tile_coords(t, type, fa, fo);
-          ss += store_grad_tile(G, net ? of.vw2 : of.w2, 64, 64, fa, fo, dw_tile<DDRL_MB>(bufA, bufB, fa, fo));
-        }
-      }
-      __syncthreads();
-      // ---- phase 2: X -> A, dZ1 -> B ; dW1 tiles, db1 ----
-      store_act(bufB, w, dz1);
+      for (int k = 0; k < NSTAT; ++k) st[k] = st0[k] + st1[k];
+    }
+    float* Pw = Pb + w * NSB;
+    // head weight / bias partial gradients over this wave's 32 rows (DPP row sums)
 #pragma unroll
-      for (int s = 0; s < 12; ++s) bufA[sidx(row_l, 4 * s + q)] = xop[s];
-      __syncthreads();
-#pragma unroll 1
-      for (int i = 0; i < 4; ++i) {
-        const int t = w + 8 * i;
-        if (t >= 20 && t < T_net) {
-          int type, fa, fo;
-          tile_coords(t, type, fa, fo);
-          ss += store_grad_tile(G, net ? of.vw1 : of.w1, 64, d, fa, fo, dw_tile<DDRL_MB>(bufA, bufB, fa, fo));
+    for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int o = 0; o < OB; ++o) {
+          const float s = row16_sum(h2[0][fb][r] * dout[0][o] + h2[1][fb][r] * dout[1][o]);
+          if (c == 0) Pw[(16 * fb + 4 * q + r) * OB + o] = s;
+        }
+#pragma unroll
+    for (int o = 0; o < OB; ++o) {
+      const float s = row16_sum(dout[0][o] + dout[1][o]);
+      if (lane == 0) Pw[64 * OB + o] = s;
+    }
+#pragma unroll
+    for (int k = 0; k < NSTAT; ++k) {
+      const float s = row16_sum(st[k]);
+      if (lane == 0) red[w * 8 + k] = s;
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      head_bwd<OB>(W, dout[t], dz[t]);
+      dtanh_inplace(dz[t], h2[t]);                       // dz = dZ2
+    }
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float s = row16_sum(dz[0][fb][r] + dz[1][fb][r]);
+        if (c == 0) Pw[64 * OB + OB + 64 + 16 * fb + 4 * q + r] = s;   // db2
+      }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      store_act(bufA, 2 * w + t, h1[t]);
+      store_act(bufB, 2 * w + t, dz[t]);
+    }
+    layer2_bwd_rt<2>(W, dz, h2);                         // h2 <- dH1
+#pragma unroll
+    for (int t = 0; t < 2; ++t) dtanh_inplace(h2[t], h1[t]);   // h2 = dZ1
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float s = row16_sum(h2[0][fb][r] + h2[1][fb][r]);
+        if (c == 0) Pw[64 * OB + OB + 16 * fb + 4 * q + r] = s;        // db1
+      }
+    __syncthreads();                                     // #1: H1, dZ2, partials visible
+    floatx4 gt[NTS];
+    dw_tile2<DDRL_MB>(bufA, bufB, tfa[0], tfo[0], tfa[1], tfo[1], gt[0], gt[1]);
+    dw_tile2<DDRL_MB>(bufA, bufB, tfa[2], tfo[2], tfa[3], tfo[3], gt[2], gt[3]);
+    __syncthreads();                                     // #2: dW2 operands consumed
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      store_act(bufB, 2 * w + t, h2[t]);
+#pragma unroll
+      for (int s = 0; s < 12; ++s) bufA[sidx(row_l[t], 4 * s + q)] = cur.x[t][s];
+    }
+    __syncthreads();                                     // #3: X, dZ1 visible
+    // ---- prefetch (the current rows are dead from here on): rows of step+1 land in `cur`
+    //      while the dW1 tiles, the norm exchange and Adam run; indices of step+2 likewise
+    if (step + 1 < last) load_row<A, KS1, POL>(U, idx_nxt, row_ok, cur);
+    if (step + 2 < last) {
+      idx_nxt[0] = row_index(U, step + 2, row_l[0], row_ok[0]);
+      idx_nxt[1] = row_index(U, step + 2, row_l[1], row_ok[1]);
+    }
+    if (tv[5]) {
+      dw_tile2<DDRL_MB>(bufA, bufB, tfa[4], tfo[4], tfa[5], tfo[5], gt[4], gt[5]);
+    } else {
+      gt[4] = tv[4] ? dw_tile<DDRL_MB>(bufA, bufB, tfa[4], tfo[4]) : splat4(0.f);
+      gt[5] = splat4(0.f);
+    }
+    gt[6] = tv[6] ? dw_tile<DDRL_MB>(bufA, bufB, tfa[6], tfo[6]) : splat4(0.f);
+    float gs[NSLOT];
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < NSLOT; ++k) {
+      const int e = tid + NT * k;
+      float s = 0.f;
+      if (e < NSB)
+        for (int i = 0; i < NW; ++i) s += Pb[i * NSB + e];
+      gs[k] = s;
+      ss += s * s;
+    }
+#pragma unroll
+    for (int i = 0; i < NTS; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int f = 16 * tfa[i] + 4 * q + r;
+        if (tv[i] && (i < NS1 || f < d)) ss += gt[i][r] * gt[i][r];
+      }
+
+    if (U.grad_out) {   // data-parallel mode: export the raw gradient of this branch
+#pragma unroll
+      for (int i = 0; i < NTS; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int f = 16 * tfa[i] + 4 * q + r, o = 16 * tfo[i] + c;
+          if (tv[i] && (i < NS1 || f < d)) U.grad_out[(i < NS1 ? bo.w2 : bo.w1) + f * 64 + o] = gt[i][r];
+        }
+#pragma unroll
+      for (int k = 0; k < NSLOT; ++k) {
+        const int e = tid + NT * k;
+        if (e < NSB) {
+          int pidx; float* lp;
+          small_param<OB>(e, bo, W, pidx, lp);
+          U.grad_out[pidx] = gs[k];
         }
       }
-      if (tid >= boff && tid < boff + 64) {
-        float s = 0.f;
-        for (int r = 0; r < DDRL_MB; ++r) s += bufB[sidx(r, tid - boff)];
-        G[(net ? of.vb1 : of.b1) + tid - boff] = s;   // db1
-        ss += s * s;
-      }
+      return;
     }
 
-    // ---- DDP: raw gradients were written to grad_out; the caller all-reduces ----
-    if (U.grad_out) return;
-
-    // ---- global norm (tf.clip_by_global_norm) ----
+    // ---- global norm: local reduction, then swap with the other branch's workgroup ----
     ss = wave_sum(ss);
-    if (lane == 0) red[w] = ss;
-    __syncthreads();   // also publishes G (workgroup scope, same CU)
+    if (lane == 0) red[64 + w] = ss;
+    __syncthreads();                                     // #4
     if (tid == 0) {
-      float tot = 0.f;
-      for (int i = 0; i < NW; ++i) tot += red[i];
+      float local = 0.f;
+      for (int i = 0; i < NW; ++i) local += red[64 + i];
+      const unsigned tag = (unsigned)step + 1u;
+      unsigned long long* mine = ub.xchg + ((size_t)p * 2 + (POL ? 0 : 1)) * 2 + (step & 1);
+      unsigned long long* other = ub.xchg + ((size_t)p * 2 + (POL ? 1 : 0)) * 2 + (step & 1);
+      __hip_atomic_store(mine, ((unsigned long long)tag << 32) | __float_as_uint(local),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned long long v;
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (true) {
+        v = __hip_atomic_load(other, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((unsigned)(v >> 32) == tag) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 300000000ull) {   // 3 s at 100 MHz
+          atomicExch(ub.err, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      const float partner = __uint_as_float((unsigned)(v & 0xffffffffu));
+      const float tot = local + partner;                 // same sum on both workgroups
       const float gn = sqrtf(tot);
-      red[16] = gn;
-      red[17] = H.grad_clip * fminf(1.f / gn, 1.f / H.grad_clip);
+      red[80] = gn;
+      red[81] = H.grad_clip * fminf(1.f / gn, 1.f / H.grad_clip);
+      if (U.stats) {
+        float sv[NSTAT];
+#pragma unroll
+        for (int k = 0; k < NSTAT; ++k) {
+          sv[k] = 0.f;
+          for (int i = 0; i < NW; ++i) sv[k] += red[i * 8 + k];
+        }
+        const float n = (float)ub.nrows;
+        float* so = U.stats + (size_t)step * 8;
+        if constexpr (POL) {
+          so[1] = sv[0] / n; so[3] = sv[1] / n; so[4] = sv[2] / n;
+          so[6] = gn; so[7] = red[81];
+        } else {
+          so[2] = sv[0] / n;
+          const float vy = sv[2] / n - (sv[1] / n) * (sv[1] / n);
+          const float vd = sv[4] / n - (sv[3] / n) * (sv[3] / n);
+          so[5] = vy > 0.f ? fmaxf(-1.f, 1.f - vd / vy) : 0.f;
+        }
+      }
     }
-    __syncthreads();
-    const float scale = red[17];
+    __syncthreads();                                     // #5
+    const float scale = red[81];
     const float alpha = H.lr * sqrtf(1.f - b2p) / (1.f - b1p);
     const float c1 = 1.f - H.b1, c2 = 1.f - H.b2;
 
-    // ---- tf1 Adam (ApplyAdam), coalesced over the flat parameter vector ----
-    for (int i = tid; i < of.n; i += NT) {
-      const float gg = G[i] * scale;
-      float mi = U.m[i], vi = U.v[i];
-      mi = mi + (gg - mi) * c1;
-      vi = vi + (gg * gg - vi) * c2;
-      U.m[i] = mi;
-      U.v[i] = vi;
-      float* lp = param_lds<O>(i, of, PW, VW);
-      *lp = *lp - (mi * alpha) / (sqrtf(vi) + H.eps);
+    // ---- tf1 Adam on owned parameters (m, v in registers, weights in LDS) ----
+#pragma unroll
+    for (int i = 0; i < NTS; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int f = 16 * tfa[i] + 4 * q + r, o = 16 * tfo[i] + c;
+        if (!(tv[i] && (i < NS1 || f < d))) continue;
+        const float g = gt[i][r] * scale;
+        mt[i][r] = mt[i][r] + (g - mt[i][r]) * c1;
+        vt4[i][r] = vt4[i][r] + (g * g - vt4[i][r]) * c2;
+        float* lp = (i < NS1 ? W.w2 : W.w1) + sidx(f, o);
+        *lp = *lp - (mt[i][r] * alpha) / (sqrtf(vt4[i][r]) + H.eps);
+      }
+#pragma unroll
+    for (int k = 0; k < NSLOT; ++k) {
+      const int e = tid + NT * k;
+      if (e >= NSB) continue;
+      int pidx; float* lp;
+      small_param<OB>(e, bo, W, pidx, lp);
+      const float g = gs[k] * scale;
+      ms[k] = ms[k] + (g - ms[k]) * c1;
+      vs[k] = vs[k] + (g * g - vs[k]) * c2;
+      *lp = *lp - (ms[k] * alpha) / (sqrtf(vs[k]) + H.eps);
     }
     b1p = b1p * H.b1;
     b2p = b2p * H.b2;
-
-    // ---- minibatch statistics (RLlib learner stats) ----
-    if (w == 0) {
-      const int n = ub.nrows;
-      float sp = 0.f, sk = 0.f, se = 0.f, sv = 0.f, st = 0.f, sy = 0.f, sd = 0.f;
-      for (int r = lane; r < n; r += 64) {
-        const float pl = scr[r], kl = scr[SCR_ROWS + r], en = scr[2 * SCR_ROWS + r];
-        const float vf = scr[3 * SCR_ROWS + r];
-        sp += pl; sk += kl; se += en; sv += vf;
-        st += pl + beta * kl + H.vf_coeff * vf - H.ent_coeff * en;
-        sy += scr[5 * SCR_ROWS + r];
-        sd += scr[5 * SCR_ROWS + r] - scr[4 * SCR_ROWS + r];
-      }
-      sp = wave_sum(sp); sk = wave_sum(sk); se = wave_sum(se); sv = wave_sum(sv);
-      st = wave_sum(st); sy = wave_sum(sy); sd = wave_sum(sd);
-      const float my = sy / n, md = sd / n;
-      float vy = 0.f, vd = 0.f;
-      for (int r = lane; r < n; r += 64) {
-        const float y = scr[5 * SCR_ROWS + r], dd = y - scr[4 * SCR_ROWS + r];
-        vy += (y - my) * (y - my);
-        vd += (dd - md) * (dd - md);
-      }
-      vy = wave_sum(vy); vd = wave_sum(vd);
-      if (lane == 0 && U.stats) {
-        float* so = U.stats + (size_t)step * 8;
-        so[0] = st / n; so[1] = sp / n; so[2] = sv / n; so[3] = sk / n; so[4] = se / n;
-        so[5] = vy > 0.f ? fmaxf(-1.f, 1.f - vd / vy) : 0.f;
-        so[6] = red[16];
-        so[7] = scale;
-      }
-    }
-    __syncthreads();
+    __syncthreads();                                     // #6: weights updated, buffers free
   }
-
-  // ---- write back weights and beta powers ----
   if (U.grad_out) return;
-  for (int i = tid; i < 48 * 64; i += NT) {
-    const int f = i >> 6, col = i & 63;
-    if (f < d) {
-      U.theta[of.w1 + i] = PW.w1[sidx(f, col)];
-      U.theta[of.vw1 + i] = VW.w1[sidx(f, col)];
+
+  // ---- write back weights, optimizer state, beta powers ----
+#pragma unroll
+  for (int i = 0; i < NTS; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = 16 * tfa[i] + 4 * q + r, o = 16 * tfo[i] + c;
+      if (!(tv[i] && (i < NS1 || f < d))) continue;
+      const int pidx = (i < NS1 ? bo.w2 : bo.w1) + f * 64 + o;
+      U.m[pidx] = mt[i][r];
+      U.v[pidx] = vt4[i][r];
     }
+#pragma unroll
+  for (int k = 0; k < NSLOT; ++k) {
+    const int e = tid + NT * k;
+    if (e >= NSB) continue;
+    int pidx; float* lp;
+    small_param<OB>(e, bo, W, pidx, lp);
+    U.m[pidx] = ms[k];
+    U.v[pidx] = vs[k];
+    U.theta[pidx] = *lp;
   }
-  for (int i = tid; i < 64 * 64; i += NT) {
-    const int f = i >> 6, col = i & 63;
-    U.theta[of.w2 + i] = PW.w2[sidx(f, col)];
-    U.theta[of.vw2 + i] = VW.w2[sidx(f, col)];
+  for (int i = tid; i < 48 * 64; i += NT) {
+    const int f = i >> 6;
+    if (f < d) U.theta[bo.w1 + i] = W.w1[sidx(f, i & 63)];
   }
-  for (int i = tid; i < 64; i += NT) {
-    U.theta[of.b1 + i] = PW.b1[i]; U.theta[of.b2 + i] = PW.b2[i];
-    U.theta[of.vb1 + i] = VW.b1[i]; U.theta[of.vb2 + i] = VW.b2[i];
-    U.theta[of.vo + i] = VW.wo[i];
-  }
-  for (int i = tid; i < 64 * O; i += NT) U.theta[of.wo + i] = PW.wo[i];
-  for (int i = tid; i < O; i += NT) U.theta[of.bo + i] = PW.bo[i];
-  if (tid == 0) {
-    U.theta[of.vbo] = VW.bo[0];
+  for (int i = tid; i < 64 * 64; i += NT) U.theta[bo.w2 + i] = W.w2[sidx(i >> 6, i & 63)];
+  if (POL && tid == 0) {
     U.beta_pow[0] = b1p;
     U.beta_pow[1] = b2p;
   }
 }
 
+template <int A, int KS1>
+__global__ void __launch_bounds__(NT) k_update_ffn(UpdateBatch ub) {
+  extern __shared__ float lds[];
+  const int p = blockIdx.x >> 1;
+  const UpdateArgs U = ub.a[p];
+  if (blockIdx.x & 1) update_loop<A, KS1, 1, false>(U, ub, lds, p);
+  else update_loop<A, KS1, 2 * A, true>(U, ub, lds, p);
+}
+
 static size_t update_lds_bytes(int O) {
-  return (size_t)(LDS_WEIGHTS_FLOATS(O) + 2 * 128 * 64 + 128 * 16 + 8 * SCR_ROWS + 32) * 4;
+  const int nsb = 64 * O + O + 128;
+  return (size_t)(BRANCH_LDS_FLOATS + 2 * 128 * 64 + NW * nsb + 128) * 4;
 }
 
 template <int A, int KS1>
 static void launch_update_t(hipStream_t s, const UpdateBatch& ub, int P) {
-  hipLaunchKernelGGL((k_update_ffn<A, KS1>), dim3(P), dim3(NT), update_lds_bytes(2 * A), s, ub);
+  hipLaunchKernelGGL((k_update_ffn<A, KS1>), dim3(2 * P), dim3(NT), update_lds_bytes(2 * A), s, ub);
 }
 
 void launch_update_ffn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHyper& h, int nrows, float inv_n,
-                       int A, int d) {
+                       int A, int d, unsigned long long* xchg, int* err) {
   UpdateBatch ub;
   ub.a = ua_dev;
   ub.h = h;
   ub.nrows = nrows;
   ub.inv_n = inv_n;
+  ub.xchg = xchg;
+  ub.err = err;
+  (void)hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * 4 * h.P, s);
   DDRL_DISPATCH_A_KS1(A, d, launch_update_t, s, ub, h.P);
 }
 
