@@ -38,7 +38,20 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, extra_flags=(), lib=None, build_dir=None) -> str:
+    """extra_flags / lib / build_dir: diagnostic variants (e.g. -DDDRL_STAMPS into
+    libddrl_hip_diag.so); the default builds the production library."""
+    global BUILD, LIB
+    BUILD_, LIB_ = BUILD, LIB
+    if lib:
+        BUILD, LIB = build_dir or BUILD + "_diag", lib
+    try:
+        return _build(force, verbose, list(extra_flags))
+    finally:
+        BUILD, LIB = BUILD_, LIB_
+
+
+def _build(force, verbose, extra_flags):
     os.makedirs(BUILD, exist_ok=True)
     headers = _headers()
     jobs = []
@@ -47,7 +60,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         objs.append(obj)
         if force or _stale(obj, [src] + headers):
-            jobs.append([HIPCC, *FLAGS, "-c", src, "-o", obj])
+            jobs.append([HIPCC, *FLAGS, *extra_flags, "-c", src, "-o", obj])
 
     def run(cmd):
         if verbose:

@@ -37,6 +37,20 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
 
 __device__ __forceinline__ floatx4 splat4(float v) { floatx4 r = {v, v, v, v}; return r; }
 
+// tanh with ~2e-7 relative error at a fraction of ocml's tanhf cost: odd Taylor series to
+// x^9 for |x| < 0.25 (truncation < 3e-9), 1 - 2 / (exp(2|x|) + 1) with the hardware
+// exp / reciprocal otherwise.  Both branches are computed and selected (no divergence).
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float ax = fabsf(x), x2 = x * x;
+  float p = fmaf(x2, 62.f / 2835.f, -17.f / 315.f);
+  p = fmaf(x2, p, 2.f / 15.f);
+  p = fmaf(x2, p, -1.f / 3.f);
+  const float small = fmaf(x * x2, p, x);
+  const float e = __expf(2.f * ax);
+  const float big = copysignf(fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f), x);
+  return ax < 0.25f ? small : big;
+}
+
 // Sum over the 4 lanes that share c (q = 0..3): fixed order ((q0+q1)+(q2+q3)).
 __device__ __forceinline__ float qsum(float v) {
   v += __shfl_xor(v, 16, 64);
@@ -62,6 +76,36 @@ __device__ __forceinline__ float row16_sum(float v) {
   v += dpp_mov<0x141>(v);  // row_half_mirror
   v += dpp_mov<0x140>(v);  // row_mirror
   return v;
+}
+
+// Transpose-reduce: v[0..15] in each lane of a DPP row (16 lanes, index c); afterwards lane c
+// holds the sum over the row of v[c].  Four exchange steps (mirror, half-mirror, quad
+// reverse, quad swap), each halving the live values: 15 DPP adds instead of 16 x 4.
+__device__ __forceinline__ float row16_transpose_sum(float v[16]) {
+  const int c = threadIdx.x & 15;
+  // step 1: partner 15-c (bit 3 differs); keep the half selected by bit 3
+  const bool b3 = c & 8, b2 = c & 4, b1 = c & 2, b0 = c & 1;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float keep = b3 ? v[8 + k] : v[k];
+    const float send = b3 ? v[k] : v[8 + k];
+    v[k] = keep + dpp_mov<0x140>(send);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float keep = b2 ? v[4 + k] : v[k];
+    const float send = b2 ? v[k] : v[4 + k];
+    v[k] = keep + dpp_mov<0x141>(send);
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const float keep = b1 ? v[2 + k] : v[k];
+    const float send = b1 ? v[k] : v[2 + k];
+    v[k] = keep + dpp_mov<0x1B>(send);   // quad_perm [3,2,1,0]
+  }
+  const float keep = b0 ? v[1] : v[0];
+  const float send = b0 ? v[0] : v[1];
+  return keep + dpp_mov<0xB1>(send);     // quad_perm [1,0,3,2]
 }
 
 __device__ __forceinline__ double wave_sum_d(double v) {
@@ -135,7 +179,7 @@ __device__ __forceinline__ void ffn_fwd_rt(const NetLds& W, const float (*xop)[1
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) h1[t][ob][r] = tanhf(h1[t][ob][r]);
+      for (int r = 0; r < 4; ++r) h1[t][ob][r] = tanh_fast(h1[t][ob][r]);
 
 #pragma unroll
   for (int ob = 0; ob < 4; ++ob) {
@@ -170,7 +214,7 @@ __device__ __forceinline__ void ffn_fwd_rt(const NetLds& W, const float (*xop)[1
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) h2[t][ob][r] = tanhf(h2[t][ob][r]);
+      for (int r = 0; r < 4; ++r) h2[t][ob][r] = tanh_fast(h2[t][ob][r]);
 
   // Linear head: partial dot over this lane's 16 features, then sum over q.
 #pragma unroll
@@ -257,6 +301,43 @@ __device__ __forceinline__ void store_act(float* buf, int tile, const floatx4 v[
     float* p = buf + wbase(r) + 1024 * tile;
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) p[16 * fb] = v[fb][r];
+  }
+}
+
+// Feature-major activation image for the weight-gradient GEMMs: T[f][b], 128 rows b per
+// feature plus 8 floats of padding (stride FM_LD = 136 == 8 mod 64 makes every ds_read_b128
+// of the dW operands bank-conflict free).  The GEMM's k index is the row b; lane (c, q)
+// takes rows 16u + 4q .. 16u + 4q + 3 for k-group u, i.e. ONE ds_read_b128 per operand per
+// four MFMAs.
+#define FM_LD 136
+__device__ __forceinline__ void store_act_fm(float* buf, int tile, const floatx4 v[4]) {
+  const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+  float* p = buf + (4 * q) * FM_LD + 16 * tile + c;
+#pragma unroll
+  for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) p[(16 * fb + r) * FM_LD] = v[fb][r];
+}
+
+// NT_ tiles dW[f = 16 fa_i + 4q + r][o = 16 fo + c] (one fo, NT_ fa's) over NROWS rows.
+template <int NROWS, int NT_>
+__device__ __forceinline__ void dw_tiles_fm(const float* A, const float* B, const int* fa, int fo, floatx4* out) {
+  const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < NT_; ++i) out[i] = splat4(0.f);
+  const float* bp = B + (16 * fo + c) * FM_LD + 4 * q;
+  const float* ap[NT_];
+#pragma unroll
+  for (int i = 0; i < NT_; ++i) ap[i] = A + (16 * fa[i] + c) * FM_LD + 4 * q;
+#pragma unroll 2
+  for (int u = 0; u < NROWS / 16; ++u) {
+    const floatx4 bv = *reinterpret_cast<const floatx4*>(bp + 16 * u);
+#pragma unroll
+    for (int i = 0; i < NT_; ++i) {
+      const floatx4 av = *reinterpret_cast<const floatx4*>(ap[i] + 16 * u);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) out[i] = mfma4(av[v], bv[v], out[i]);
+    }
   }
 }
 

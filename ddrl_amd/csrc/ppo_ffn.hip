@@ -58,7 +58,7 @@ __device__ void stage_branch(const float* __restrict__ th, int d, const BranchOf
   for (int i = threadIdx.x; i < 64 * OB; i += NT) W.wo[i] = th[bo.wo + i];
   for (int i = threadIdx.x; i < OB; i += NT) W.bo[i] = th[bo.bo + i];
 }
-#define BRANCH_LDS_FLOATS (48 * 64 + 64 * 64 + 128 + 64 * 16 + 16)
+#define BRANCH_LDS_FLOATS (48 * 64 + 64 * 64 + 128 + 64 * 16 + 16)   // multiple of 4 floats
 
 // "Small" parameters owned one per thread: [dWo 64*OB][dbo OB][db1 64][db2 64]
 template <int OB>
@@ -114,26 +114,32 @@ __device__ __forceinline__ int row_index(const UpdateArgs& U, int step, int row_
   const int e = step / U.nb, b = step - e * U.nb;
   return U.shuffle[U.perm[e * U.nb + b] * DDRL_MB + row_l];
 }
+// minibatch slot of a step (wave-uniform: perm[e][b])
+__device__ __forceinline__ int perm_slot(const UpdateArgs& U, int step) {
+  const int e = step / U.nb, b = step - e * U.nb;
+  return U.perm[e * U.nb + b];
+}
 
 // Per-row PPO loss terms and output gradient (policy branch).
 template <int A>
 __device__ __forceinline__ void policy_loss_row(const float* out, const float* act, const float* ol,
                                                 float logp_old, float adv, float beta, float lo, float hi,
                                                 float ent_coeff, float inv_n, bool ok, float* dout, float* st) {
+  // hardware exp / no divisions: 1 / sd = exp(-log_std), sd_old^2 = exp(2 log_std_old)
   float logp = -0.5f * (float)(DDRL_LOG2PI * A), klr = 0.f, ent = 0.f;
-  float z[A], sd[A];
+  float z[A], isd[A], q0[A];
 #pragma unroll
   for (int j = 0; j < A; ++j) {
-    sd[j] = expf(out[A + j]);
-    z[j] = (act[j] - out[j]) / sd[j];
+    isd[j] = __expf(-out[A + j]);
+    z[j] = (act[j] - out[j]) * isd[j];
     logp -= 0.5f * z[j] * z[j];
     logp -= out[A + j];
-    const float v0 = expf(ol[A + j]);
     const float dm = ol[j] - out[j];
-    klr += out[A + j] - ol[A + j] + (v0 * v0 + dm * dm) / (2.f * sd[j] * sd[j]) - 0.5f;
+    q0[j] = __expf(2.f * ol[A + j]) + dm * dm;
+    klr += out[A + j] - ol[A + j] + 0.5f * q0[j] * (isd[j] * isd[j]) - 0.5f;
     ent += out[A + j] + 0.5f * (float)(DDRL_LOG2PI + 1.0);
   }
-  const float ratio = expf(logp - logp_old);
+  const float ratio = __expf(logp - logp_old);
   const float cr = fminf(fmaxf(ratio, lo), hi);
   const float s1 = adv * ratio, s2 = adv * cr;
   const float surr = fminf(s1, s2);
@@ -141,11 +147,9 @@ __device__ __forceinline__ void policy_loss_row(const float* out, const float* a
   const float glogp = -dr * ratio;
 #pragma unroll
   for (int j = 0; j < A; ++j) {
-    const float v0 = expf(ol[A + j]);
-    const float dm = ol[j] - out[j];
-    const float var1 = sd[j] * sd[j];
-    const float dmu = glogp * (z[j] / sd[j]) + beta * ((out[j] - ol[j]) / var1);
-    const float dls = glogp * (z[j] * z[j] - 1.f) + beta * (1.f - (v0 * v0 + dm * dm) / var1) - ent_coeff;
+    const float iv = isd[j] * isd[j];
+    const float dmu = glogp * (z[j] * isd[j]) + beta * ((out[j] - ol[j]) * iv);
+    const float dls = glogp * (z[j] * z[j] - 1.f) + beta * (1.f - q0[j] * iv) - ent_coeff;
     dout[j] = ok ? dmu * inv_n : 0.f;
     dout[A + j] = ok ? dls * inv_n : 0.f;
   }
@@ -180,6 +184,22 @@ __device__ __forceinline__ void value_loss_row(float V, float vfo, float vtg, co
   st[4] = ok ? dd * dd : 0.f;
 }
 
+// Diagnostic build only (-DDDRL_STAMPS): per-phase s_memtime cycle counts of wave 0 of each
+// workgroup, accumulated over the steps of one launch; no stamp executes in the real build.
+#ifdef DDRL_STAMPS
+__device__ unsigned long long g_stamps[2 * DDRL_MAXP][16];
+#define STAMP_INIT unsigned long long st_prev = __builtin_amdgcn_s_memtime(), st_acc[12] = {0};
+#define STAMP(k) do { if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[k] += t_ - st_prev; st_prev = t_; } } while (0)
+#define STAMP_DONE do { if (tid == 0) for (int k_ = 0; k_ < 12; ++k_) g_stamps[blockIdx.x][k_] = st_acc[k_]; } while (0)
+extern "C" int ddrl_diag_stamps(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) == hipSuccess ? 0 : -1;
+}
+#else
+#define STAMP_INIT
+#define STAMP(k)
+#define STAMP_DONE
+#endif
+
 #define NS1 4   // dW2 tile slots per wave (16 tiles / 4 waves)
 #define NS2 3   // dW1 tile slots per wave (<= 12 tiles / 4 waves)
 
@@ -197,9 +217,9 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 
   NetLds W;
   stage_branch<OB>(U.theta, d, bo, lds, W);
-  float* bufA = lds + BRANCH_LDS_FLOATS;
-  float* bufB = bufA + 128 * 64;
-  float* Pb = bufB + 128 * 64;              // [NW][NSB] per-wave partial small grads
+  float* bufA = lds + BRANCH_LDS_FLOATS;    // feature-major [64][FM_LD]: H1, then X
+  float* bufB = bufA + 64 * FM_LD;          // feature-major [64][FM_LD]: dZ2, then dZ1
+  float* Pb = bufB + 64 * FM_LD;            // [NW][NSB] per-wave partial small grads
   float* red = Pb + NW * NSB;               // [NW][8] row-stat partials, [64..] scalars
 
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, q = lane >> 4, w = tid >> 6;
@@ -243,6 +263,9 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       vs[k] = U.v[pidx];
     }
   }
+  int ebase[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) ebase[r] = sidx(4 * q + r, 16 * w + c);
   float b1p = U.beta_pow[0], b2p = U.beta_pow[1];
   const float adv_mean = U.adv_norm[0], adv_den = U.adv_norm[1];
   const float beta = U.kl_coeff;
@@ -253,6 +276,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   const int last = U.max_steps >= 0 ? min(total_steps, U.step0 + U.max_steps) : total_steps;
   RowData<A> cur;
   int idx_nxt[2] = {0, 0};
+  int slot_nn = 0;   // perm slot of step+2, loaded one step before its shuffle lookup
   if (U.step0 < last) {
     int ix[2] = {row_index(U, U.step0, row_l[0], row_ok[0]), row_index(U, U.step0, row_l[1], row_ok[1])};
     load_row<A, KS1, POL>(U, ix, row_ok, cur);
@@ -261,13 +285,15 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     idx_nxt[0] = row_index(U, U.step0 + 1, row_l[0], row_ok[0]);
     idx_nxt[1] = row_index(U, U.step0 + 1, row_l[1], row_ok[1]);
   }
+  if (U.step0 + 2 < last) slot_nn = perm_slot(U, U.step0 + 2);
 
+  STAMP_INIT
   for (int step = U.step0; step < last; ++step) {
-
     // ---- forward + loss + output gradient (two row tiles) ----
     floatx4 h1[2][4], h2[2][4], dz[2][4];
     float out[2][OB], dout[2][OB];
     ffn_fwd_rt<OB, KS1, 2>(W, cur.x, h1, h2, out);
+    STAMP(0);
     float st[NSTAT];
     {
       float st0[NSTAT], st1[NSTAT];
@@ -283,17 +309,21 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 #pragma unroll
       for (int k = 0; k < NSTAT; ++k) st[k] = st0[k] + st1[k];
     }
+    STAMP(1);
     float* Pw = Pb + w * NSB;
-    // head weight / bias partial gradients over this wave's 32 rows (DPP row sums)
+    // head weight / bias partial gradients over this wave's 32 rows: DPP transpose-reduce
+    // of the 16 features (fb, r) a lane holds; afterwards lane (c, q) owns feature
+    // h = 16 (c >> 2) + 4 q + (c & 3).
+    const int h_own = 16 * (c >> 2) + 4 * q + (c & 3);
 #pragma unroll
-    for (int fb = 0; fb < 4; ++fb)
+    for (int o = 0; o < OB; ++o) {
+      float v[16];
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+      for (int fb = 0; fb < 4; ++fb)
 #pragma unroll
-        for (int o = 0; o < OB; ++o) {
-          const float s = row16_sum(h2[0][fb][r] * dout[0][o] + h2[1][fb][r] * dout[1][o]);
-          if (c == 0) Pw[(16 * fb + 4 * q + r) * OB + o] = s;
-        }
+        for (int r = 0; r < 4; ++r) v[4 * fb + r] = h2[0][fb][r] * dout[0][o] + h2[1][fb][r] * dout[1][o];
+      Pw[h_own * OB + o] = row16_transpose_sum(v);
+    }
 #pragma unroll
     for (int o = 0; o < OB; ++o) {
       const float s = row16_sum(dout[0][o] + dout[1][o]);
@@ -304,59 +334,70 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       const float s = row16_sum(st[k]);
       if (lane == 0) red[w * 8 + k] = s;
     }
+    STAMP(2);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       head_bwd<OB>(W, dout[t], dz[t]);
       dtanh_inplace(dz[t], h2[t]);                       // dz = dZ2
     }
+    {
+      float v[16];
 #pragma unroll
-    for (int fb = 0; fb < 4; ++fb)
+      for (int fb = 0; fb < 4; ++fb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float s = row16_sum(dz[0][fb][r] + dz[1][fb][r]);
-        if (c == 0) Pw[64 * OB + OB + 64 + 16 * fb + 4 * q + r] = s;   // db2
-      }
+        for (int r = 0; r < 4; ++r) v[4 * fb + r] = dz[0][fb][r] + dz[1][fb][r];
+      Pw[64 * OB + OB + 64 + h_own] = row16_transpose_sum(v);     // db2
+    }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      store_act(bufA, 2 * w + t, h1[t]);
-      store_act(bufB, 2 * w + t, dz[t]);
+      store_act_fm(bufA, 2 * w + t, h1[t]);
+      store_act_fm(bufB, 2 * w + t, dz[t]);
     }
+    STAMP(3);
     layer2_bwd_rt<2>(W, dz, h2);                         // h2 <- dH1
 #pragma unroll
     for (int t = 0; t < 2; ++t) dtanh_inplace(h2[t], h1[t]);   // h2 = dZ1
+    {
+      float v[16];
 #pragma unroll
-    for (int fb = 0; fb < 4; ++fb)
+      for (int fb = 0; fb < 4; ++fb)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float s = row16_sum(h2[0][fb][r] + h2[1][fb][r]);
-        if (c == 0) Pw[64 * OB + OB + 16 * fb + 4 * q + r] = s;        // db1
-      }
+        for (int r = 0; r < 4; ++r) v[4 * fb + r] = h2[0][fb][r] + h2[1][fb][r];
+      Pw[64 * OB + OB + h_own] = row16_transpose_sum(v);          // db1
+    }
+    STAMP(4);
     __syncthreads();                                     // #1: H1, dZ2, partials visible
+    STAMP(5);
     floatx4 gt[NTS];
-    dw_tile2<DDRL_MB>(bufA, bufB, tfa[0], tfo[0], tfa[1], tfo[1], gt[0], gt[1]);
-    dw_tile2<DDRL_MB>(bufA, bufB, tfa[2], tfo[2], tfa[3], tfo[3], gt[2], gt[3]);
+    {
+      const int fa4[4] = {0, 1, 2, 3};
+      dw_tiles_fm<DDRL_MB, 4>(bufA, bufB, fa4, w, gt);   // dW2 tiles (fa = 0..3, fo = w)
+    }
+    STAMP(6);
     __syncthreads();                                     // #2: dW2 operands consumed
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      store_act(bufB, 2 * w + t, h2[t]);
+      store_act_fm(bufB, 2 * w + t, h2[t]);
 #pragma unroll
-      for (int s = 0; s < 12; ++s) bufA[sidx(row_l[t], 4 * s + q)] = cur.x[t][s];
+      for (int s = 0; s < 12; ++s) bufA[(4 * s + q) * FM_LD + row_l[t]] = cur.x[t][s];
     }
     __syncthreads();                                     // #3: X, dZ1 visible
     // ---- prefetch (the current rows are dead from here on): rows of step+1 land in `cur`
     //      while the dW1 tiles, the norm exchange and Adam run; indices of step+2 likewise
     if (step + 1 < last) load_row<A, KS1, POL>(U, idx_nxt, row_ok, cur);
-    if (step + 2 < last) {
-      idx_nxt[0] = row_index(U, step + 2, row_l[0], row_ok[0]);
-      idx_nxt[1] = row_index(U, step + 2, row_l[1], row_ok[1]);
+    if (step + 2 < last) {   // slot_nn arrived during the previous step: no dependent wait
+      idx_nxt[0] = row_ok[0] ? U.shuffle[slot_nn * DDRL_MB + row_l[0]] : 0;
+      idx_nxt[1] = row_ok[1] ? U.shuffle[slot_nn * DDRL_MB + row_l[1]] : 0;
     }
-    if (tv[5]) {
-      dw_tile2<DDRL_MB>(bufA, bufB, tfa[4], tfo[4], tfa[5], tfo[5], gt[4], gt[5]);
-    } else {
-      gt[4] = tv[4] ? dw_tile<DDRL_MB>(bufA, bufB, tfa[4], tfo[4]) : splat4(0.f);
-      gt[5] = splat4(0.f);
+    if (step + 3 < last) slot_nn = perm_slot(U, step + 3);
+    {
+      const int fa3[3] = {0, 1, 2};                     // dW1 tiles (fa < nf1, fo = w)
+      gt[4] = gt[5] = gt[6] = splat4(0.f);
+      if (nf1 >= 3) dw_tiles_fm<DDRL_MB, 3>(bufA, bufB, fa3, w, gt + 4);
+      else if (nf1 == 2) dw_tiles_fm<DDRL_MB, 2>(bufA, bufB, fa3, w, gt + 4);
+      else dw_tiles_fm<DDRL_MB, 1>(bufA, bufB, fa3, w, gt + 4);
     }
-    gt[6] = tv[6] ? dw_tile<DDRL_MB>(bufA, bufB, tfa[6], tfo[6]) : splat4(0.f);
+    STAMP(7);
     float gs[NSLOT];
     float ss = 0.f;
 #pragma unroll
@@ -424,59 +465,86 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       const float gn = sqrtf(tot);
       red[80] = gn;
       red[81] = H.grad_clip * fminf(1.f / gn, 1.f / H.grad_clip);
-      if (U.stats) {
-        float sv[NSTAT];
-#pragma unroll
-        for (int k = 0; k < NSTAT; ++k) {
-          sv[k] = 0.f;
-          for (int i = 0; i < NW; ++i) sv[k] += red[i * 8 + k];
-        }
-        const float n = (float)ub.nrows;
-        float* so = U.stats + (size_t)step * 8;
-        if constexpr (POL) {
-          so[1] = sv[0] / n; so[3] = sv[1] / n; so[4] = sv[2] / n;
-          so[6] = gn; so[7] = red[81];
-        } else {
-          so[2] = sv[0] / n;
-          const float vy = sv[2] / n - (sv[1] / n) * (sv[1] / n);
-          const float vd = sv[4] / n - (sv[3] / n) * (sv[3] / n);
-          so[5] = vy > 0.f ? fmaxf(-1.f, 1.f - vd / vy) : 0.f;
-        }
-      }
     }
     __syncthreads();                                     // #5
+    STAMP(8);
+    if (U.stats && tid == 64) {   // off the critical path: wave 1, after the exchange
+      float sv[NSTAT];
+#pragma unroll
+      for (int k = 0; k < NSTAT; ++k) {
+        sv[k] = 0.f;
+        for (int i = 0; i < NW; ++i) sv[k] += red[i * 8 + k];
+      }
+      const float n = (float)ub.nrows;
+      float* so = U.stats + (size_t)step * 8;
+      if constexpr (POL) {
+        so[1] = sv[0] / n; so[3] = sv[1] / n; so[4] = sv[2] / n;
+        so[6] = red[80]; so[7] = red[81];
+      } else {
+        so[2] = sv[0] / n;
+        const float vy = sv[2] / n - (sv[1] / n) * (sv[1] / n);
+        const float vd = sv[4] / n - (sv[3] / n) * (sv[3] / n);
+        so[5] = vy > 0.f ? fmaxf(-1.f, 1.f - vd / vy) : 0.f;
+      }
+    }
     const float scale = red[81];
     const float alpha = H.lr * sqrtf(1.f - b2p) / (1.f - b1p);
     const float c1 = 1.f - H.b1, c2 = 1.f - H.b2;
 
     // ---- tf1 Adam on owned parameters (m, v in registers, weights in LDS) ----
+    // element (f = 16 fa + 4q + r, o = 16 w + c) sits at ebase[r] + 1024 fa in W1 / W2.
+    // All owned weights are read first, then updated, then written (no read-after-write
+    // ordering between different parameters' LDS words).
+    {
+      float th[NTS][4], ts[NSLOT];
 #pragma unroll
-    for (int i = 0; i < NTS; ++i)
+      for (int i = 0; i < NTS; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int f = 16 * tfa[i] + 4 * q + r, o = 16 * tfo[i] + c;
-        if (!(tv[i] && (i < NS1 || f < d))) continue;
-        const float g = gt[i][r] * scale;
-        mt[i][r] = mt[i][r] + (g - mt[i][r]) * c1;
-        vt4[i][r] = vt4[i][r] + (g * g - vt4[i][r]) * c2;
-        float* lp = (i < NS1 ? W.w2 : W.w1) + sidx(f, o);
-        *lp = *lp - (mt[i][r] * alpha) / (sqrtf(vt4[i][r]) + H.eps);
+        for (int r = 0; r < 4; ++r)
+          th[i][r] = (i < NS1 ? W.w2 : W.w1)[ebase[r] + 1024 * (i < NS1 ? i : i - NS1)];
+#pragma unroll
+      for (int k = 0; k < NSLOT; ++k) {
+        const int e = tid + NT * k;
+        ts[k] = 0.f;
+        if (e < NSB) { int pidx; float* lp; small_param<OB>(e, bo, W, pidx, lp); ts[k] = *lp; }
       }
 #pragma unroll
-    for (int k = 0; k < NSLOT; ++k) {
-      const int e = tid + NT * k;
-      if (e >= NSB) continue;
-      int pidx; float* lp;
-      small_param<OB>(e, bo, W, pidx, lp);
-      const float g = gs[k] * scale;
-      ms[k] = ms[k] + (g - ms[k]) * c1;
-      vs[k] = vs[k] + (g * g - vs[k]) * c2;
-      *lp = *lp - (ms[k] * alpha) / (sqrtf(vs[k]) + H.eps);
+      for (int i = 0; i < NTS; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float g = gt[i][r] * scale;
+          mt[i][r] = mt[i][r] + (g - mt[i][r]) * c1;
+          vt4[i][r] = vt4[i][r] + (g * g - vt4[i][r]) * c2;
+          th[i][r] = th[i][r] - (mt[i][r] * alpha) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vt4[i][r]) + H.eps);
+        }
+#pragma unroll
+      for (int k = 0; k < NSLOT; ++k) {
+        const float g = gs[k] * scale;
+        ms[k] = ms[k] + (g - ms[k]) * c1;
+        vs[k] = vs[k] + (g * g - vs[k]) * c2;
+        ts[k] = ts[k] - (ms[k] * alpha) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vs[k]) + H.eps);
+      }
+#pragma unroll
+      for (int i = 0; i < NTS; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int f = 16 * tfa[i] + 4 * q + r;
+          if (tv[i] && (i < NS1 || f < d))
+            (i < NS1 ? W.w2 : W.w1)[ebase[r] + 1024 * (i < NS1 ? i : i - NS1)] = th[i][r];
+        }
+#pragma unroll
+      for (int k = 0; k < NSLOT; ++k) {
+        const int e = tid + NT * k;
+        if (e < NSB) { int pidx; float* lp; small_param<OB>(e, bo, W, pidx, lp); *lp = ts[k]; }
+      }
     }
     b1p = b1p * H.b1;
     b2p = b2p * H.b2;
+    STAMP(9);
     __syncthreads();                                     // #6: weights updated, buffers free
+    STAMP(10);
   }
+  STAMP_DONE;
   if (U.grad_out) return;
 
   // ---- write back weights, optimizer state, beta powers ----
@@ -522,7 +590,7 @@ __global__ void __launch_bounds__(NT) k_update_ffn(UpdateBatch ub) {
 
 static size_t update_lds_bytes(int O) {
   const int nsb = 64 * O + O + 128;
-  return (size_t)(BRANCH_LDS_FLOATS + 2 * 128 * 64 + NW * nsb + 128) * 4;
+  return (size_t)(BRANCH_LDS_FLOATS + 2 * 64 * FM_LD + NW * nsb + 128) * 4;
 }
 
 template <int A, int KS1>

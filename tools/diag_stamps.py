@@ -1,0 +1,42 @@
+"""Per-phase cycle breakdown of the fused update kernel (diagnostic build with s_memtime
+stamps; only the shares are meaningful, the stamps themselves cost a little)."""
+import ctypes, os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np, torch
+from ddrl_amd import build, native as N
+lib = build.build(extra_flags=["-DDDRL_STAMPS"], lib=os.path.join(os.path.dirname(N.LIB_PATH), "libddrl_hip_diag.so"))
+N.load(lib)
+from ddrl_amd.spec import make_cfg
+from ddrl_amd.trainer import glorot_ffn_flat
+n, T = int(sys.argv[1]) if len(sys.argv) > 1 else 512, 200
+cfg, inst = make_cfg("QuantrupedMultiEnv_Local", n, T)
+ctx = N.Context(cfg, 0, torch.cuda.current_stream().cuda_stream)
+rng = np.random.default_rng(0)
+for p in range(4):
+    ctx.params_set(p, glorot_ffn_flat(rng, 35, 2))
+recs = []
+for p in range(4):
+    lay = ctx.layout[p]
+    r = rng.normal(size=(T * lay["C"], lay["stride"])).astype(np.float32) * 0.5
+    r[:, lay["logit"] + 2:lay["logit"] + 4] = -0.5
+    ctx.records_set(p, r)
+R = T * n; nb = R // 128
+sh = [torch.from_numpy(rng.permutation(R).astype(np.int32)).cuda() for _ in range(4)]
+pe = [torch.from_numpy(np.stack([rng.permutation(nb) for _ in range(10)]).astype(np.int32)).cuda() for _ in range(4)]
+steps = 10 * nb
+for it in range(2):
+    t0 = time.perf_counter()
+    ctx.ppo_update(0xF, sh, pe, [0.2] * 4)
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+st = (ctypes.c_ulonglong * (8 * 16))()
+assert N.load().ddrl_diag_stamps(st) == 0
+a = np.array(st, dtype=np.float64).reshape(8, 16)[:, :11] / steps
+names = ["fwd", "loss", "dpp head/bias", "head bwd+db2+stores", "layer2 bwd+db1", "sync#1",
+         "dW2 tiles", "sync#2,#3+X/dZ1 stores+dW1 tiles+prefetch", "norm+exchange", "adam", "sync#6"]
+print(f"steps {steps}, {dt / steps * 1e6:.2f} us/step wall")
+for wg in (0, 1):
+    tot = a[wg].sum()
+    print(("policy" if wg == 0 else "value ") + f" WG: {tot:.0f} cycles/step")
+    for k, nm in enumerate(names):
+        print(f"   {nm:45s} {a[wg, k]:8.0f}  {100 * a[wg, k] / tot:5.1f}%")
