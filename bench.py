@@ -32,6 +32,20 @@ sys.path.insert(0, ROOT)
 METRIC = "env-steps/sec at 4096 envs × 4 leg agents; PPO update ms/minibatch"
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense FP32 (MFMA f32 = vector rate), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "pmc_update.json")
+
+
+def pmc_traffic(kernel_name, policy_steps):
+    """HBM bytes per launch of the update kernel from the committed rocprofv3 PMC passes
+    (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE; tools/profile_r01.sh), per
+    (policy, minibatch) step times this launch's steps -- the kernel's traffic is per step.
+    The counters cannot be read live from inside the timed run; None if no summary matches."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            s = json.load(f)
+    except OSError:
+        return None
+    return s["hbm_bytes_per_policy_step"] * policy_steps if kernel_name in s.get("kernel", "") else None
 
 
 def ffn_flops_per_row(d, A, H=64):
@@ -113,7 +127,7 @@ def main():
     ap.add_argument("--env", default="QuantrupedMultiEnv_Local")
     ap.add_argument("--frag", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-envs", type=int, default=128)
+    ap.add_argument("--cpu-envs", type=int, default=512)
     args = ap.parse_args()
 
     import torch
@@ -210,6 +224,12 @@ def main():
     d = cfg.obs_dim[0]
     flops_launch = ffn_flops_per_row(d, A) * 128 * steps_per_policy * P
     achieved_tf = flops_launch / (upd_avg_ms * 1e-3) / 1e12
+    # one launch keeps 2 workgroups (policy / value branch) per policy resident, one per CU:
+    # the per-CU fraction is the achieved rate over the MFMA peak of the CUs it occupies
+    active_cus = 2 * P
+    # algorithmic HBM bytes: each minibatch row's record fields read once per branch
+    # (policy: obs, action, old logits, logp, adv; value: obs, vf, vt) + its shuffle index
+    rec_bytes_launch = 4 * (2 * d + 3 * A + 4 + 2) * 128 * steps_per_policy * P
     result = {
         "metric": METRIC,
         "value": env_steps / t_max,
@@ -235,8 +255,12 @@ def main():
         "roofline": {
             "kernel": "k_update_ffn (fused PPO minibatch SGD, one launch per iteration)",
             "bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-            "frac": achieved_tf / PEAK_FP32_TFLOPS, "traffic": None,
+            "frac": achieved_tf / PEAK_FP32_TFLOPS,
+            "traffic": pmc_traffic(f"k_update_ffn<{A}, ", steps_per_policy * P),
             "algorithmic_flops_per_launch": flops_launch,
+            "algorithmic_bytes_per_launch": rec_bytes_launch,
+            "active_cus": active_cus,
+            "frac_of_active_cus": achieved_tf / (PEAK_FP32_TFLOPS * active_cus / 256),
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
