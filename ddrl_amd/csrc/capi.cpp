@@ -30,10 +30,7 @@ int fail(const std::string& msg) {
   if (!(c)) return fail("null context")
 
 int ffn_param_count(int d, int A) { return d * 64 * 2 + 128 + 2 * 4096 + 128 + 64 * 2 * A + 2 * A + 65; }
-int gnn_param_count(int A) {
-  const int net = 4 * 1216 + 1216 + 2 * 4096;
-  return net + 64 * 2 * A + 2 * A + net + 64 + 1;
-}
+int gnn_param_count(int A) { return gnn_param_total(A); }
 
 struct Policy {
   int k = 0, d = 0, C = 0, n_params = 0, R = 0, nb = 0;
@@ -61,6 +58,7 @@ struct ddrl_ctx {
   unsigned long long* xchg = nullptr;  // norm^2 exchange granules of the update kernel
   int* err = nullptr;                  // device error word (exchange timeout)
   float kl_last[DDRL_MAXP] = {0};
+  GnnScratch gnn{};               // GraphNet step scratch (per-tile partial gradients, ...)
   // host-variant staging
   float *h_obs = nullptr, *h_eps = nullptr, *h_act = nullptr;
   std::vector<void*> allocs;
@@ -112,6 +110,7 @@ static int validate(const ddrl_cfg& c) {
   }
   if (c.model_kind == DDRL_MODEL_GNN && (c.n_policies != 1 || c.n_agents != 4 || c.obs_dim[0] != 19))
     return fail("gnn requires one shared leg policy, 4 agents and 19 features per node");
+  if (c.model_kind == DDRL_MODEL_GNN && c.act_dim != 2) return fail("gnn kernels are built for act_dim 2");
   for (int j = 0; j < c.n_agents; ++j) {
     const int d = c.obs_dim[c.agent_policy[j]];
     for (int f = 0; f < d; ++f)
@@ -185,6 +184,13 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
        dalloc(c, &c->d_uargs, DDRL_MAXP) || dalloc(c, &c->xchg, 4 * DDRL_MAXP) || dalloc(c, &c->err, 1) ||
        dalloc(c, &c->h_obs, (size_t)N * g.obs_full_dim) ||
        dalloc(c, &c->h_eps, (size_t)N * g.n_agents * g.act_dim) || dalloc(c, &c->h_act, (size_t)N * 8);
+  if (!rc && g.model_kind == DDRL_MODEL_GNN) {
+    const int np = c->pol[0].n_params;
+    c->gnn.part_stride = np;
+    c->gnn.grad = c->pol[0].grad;
+    rc = dalloc(c, &c->gnn.part, (size_t)(DDRL_MB / 4) * np) || dalloc(c, &c->gnn.statp, 2 * (DDRL_MB / 4) * 8) ||
+         dalloc(c, &c->gnn.normp, (np + 255) / 256) || dalloc(c, &c->gnn.bp_cur, 2);
+  }
   if (!rc) {
     float* tab[DDRL_MAXP] = {nullptr};
     for (int p = 0; p < g.n_policies; ++p) tab[p] = c->pol[p].stage;
@@ -461,7 +467,8 @@ int ddrl_ppo_update(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const 
     launch_update_ffn(c->stream, c->d_uargs, h, 128, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim, maxd,
                       c->xchg, c->err);
   else
-    launch_update_gnn(c->stream, c->d_uargs, h, 128, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim);
+    for (int step = 0; step < c->pol[0].last_steps; ++step)   // one shared policy
+      launch_step_gnn(c->stream, ua[0], h, step, 128, 1.f / c->cfg.sgd_minibatch_size, c->gnn);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -498,7 +505,7 @@ int ddrl_ppo_grad(ddrl_ctx* c, int pid, const int32_t* rows, int n_rows, float k
     launch_update_ffn(c->stream, c->d_uargs, h, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim,
                       c->pol[pid].d, c->xchg, c->err);
   else
-    launch_update_gnn(c->stream, c->d_uargs, h, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim);
+    launch_step_gnn(c->stream, u, h, 0, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->gnn);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -518,6 +525,7 @@ int ddrl_policy_forward(ddrl_ctx* c, int pid, const float* obs, const int32_t* n
   CHK_CTX(c);
   if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
   if (n < 1 || !obs || !logits || !values) return fail("bad forward arguments");
+  if (c->cfg.model_kind == DDRL_MODEL_GNN && !node) return fail("gnn forward needs the node index of every row");
   Policy& P = c->pol[pid];
   ForwardArgs fa{};
   fa.theta = P.theta; fa.x = obs; fa.node = node; fa.n = n; fa.d = P.d; fa.A = c->cfg.act_dim;

@@ -25,7 +25,9 @@
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 #define DDRL_H 64          // hidden width (fcnet_hiddens = [64, 64])
+#ifndef DDRL_MB
 #define DDRL_MB 128        // sgd_minibatch_size supported by the fused update kernel
+#endif
 #define DDRL_LOG2PI 1.8378770664093453
 
 __device__ __forceinline__ int swz(int row) { return ((row >> 1) & 7) << 1; }

@@ -1,7 +1,537 @@
-// GraphNet / MPNN ("gnn") kernels -- placeholder launchers until the GNN path lands.
+// a3/a9/a10 + a13-a16 for the GraphNet / MPNN model ("gnn", shared leg policy).
+//
+// Reference: models/graph_net.py:8-45 (GraphNet: hypernetwork state encoder + MPNN + linear
+// out), models/gcn.py:57-94 (MPNN: message = h Wmsg, segment-mean over receivers,
+// y = tanh(h Wnode + m)), models/shared_graphnet_glorot_uniform_init.py:14-58 (actor and
+// critic are two separate GraphNets on the same graph observation; the agent's own node
+// is gathered before linear_out).  Per net and node n of a graph:
+//   W_n = tanh(q_n Wenc + benc)  reshaped [19, 64]      (q_n = ego quaternion, 4)
+//   h_n = tanh(f_n W_n)                                  (f_n = 19 leg features)
+//   m_n = (h_{n-1} Wmsg + h_{n+1} Wmsg) / 2              (ring FL-HL-HR-FR)
+//   y_n = tanh(h_n Wnode + m_n);  out = y_sel Wout + bout
+//
+// Work unit: one workgroup = one TILE of 4 graphs x 4 nodes (16 graph-nodes, the 16 rows
+// of a 16x16x4 f32 MFMA) for ONE net (blockIdx.y = 0 actor, 1 critic).  Lane (c, q) of
+// every wave owns graph-node row c = 4 g + n; activations live in registers in the
+// transposed MFMA layout (row c, features 16 t + 4 q + r), as in the fcnet kernels.
+//   hypernet : the 4 waves split the 19 feature rows i of W_n (i = w, w+4, ...); for each
+//              (i, 16-column block t) one MFMA (K = 4 quaternion dims, bias in the
+//              accumulator), tanh, and f_i * W_n[i] accumulated in registers; the four
+//              partial sums meet in LDS (fixed order) -> h.
+//   MPNN     : wave w computes output features 16 w .. 16 w + 15 of msg and node from h in
+//              registers (A = weights, loaded once per launch into VGPRs); the ring
+//              neighbours of a node are the other lanes of its DPP quad (quad_perm).
+//   head     : per-wave partial dot over its 16 features, summed across waves in LDS.
+//   backward : the reverse of the above; weight gradients of Wmsg / Wnode as 16x16 tiles
+//              over the 16 rows (MFMA, LDS images), Wenc / benc / Wout gradients by DPP
+//              transpose-reductions over the 16 rows of a DPP row.
+// Training steps are three launches: per-tile partial gradients (k_gnn<MODE_GRAD>), a
+// fixed-order reduction over tiles + squared norm partials (k_gnn_reduce), and
+// clip_by_global_norm + tf1 Adam (k_gnn_adam).  A DDP step stops after the reduction.
 #include "common.h"
 #include "kernels.h"
+#include "ppo_loss.h"
 
-void launch_act_gnn(hipStream_t, const RouteArgs&, const ActArgs&) {}
-void launch_update_gnn(hipStream_t, const UpdateArgs*, const UpdateHyper&, int, float, int) {}
-void launch_forward_gnn(hipStream_t, const ForwardArgs&) {}
+#define GF 19              // leg features per node
+#define GHE (GF * 64)      // hypernetwork output width (1216)
+#define GNI 5              // feature rows i per wave (ceil(19 / 4))
+
+enum { GNN_ACT = 0, GNN_FWD = 1, GNN_GRAD = 2 };
+
+struct GnnNetOff { int wenc, benc, wmsg, wnode, wout, bout; };
+__host__ __device__ inline GnnNetOff gnn_net_off(int A, int net) {
+  const int actor = 4 * GHE + GHE + 2 * 4096 + 64 * 2 * A + 2 * A;
+  const int O = net ? 1 : 2 * A;
+  GnnNetOff o;
+  o.wenc = net ? actor : 0;
+  o.benc = o.wenc + 4 * GHE;
+  o.wmsg = o.benc + GHE;
+  o.wnode = o.wmsg + 4096;
+  o.wout = o.wnode + 4096;
+  o.bout = o.wout + 64 * O;
+  return o;
+}
+
+// DPP quad neighbours: lane n of a quad receives lane (n - 1) & 3 / (n + 1) & 3.
+__device__ __forceinline__ float quad_prev(float v) { return dpp_mov<0x93>(v); }   // [3,0,1,2]
+__device__ __forceinline__ float quad_next(float v) { return dpp_mov<0x39>(v); }   // [1,2,3,0]
+
+// LDS (floats): part [4 waves][16][64] (hypernet partials; later dz exchange), h / du / dm
+// images [16][64] swizzled, head partials [4][16][4], per-graph dout [4][4], stats [4][8].
+#define L_PART 0
+#define L_H (L_PART + 4096)
+#define L_DU (L_H + 1024)
+#define L_DM (L_DU + 1024)
+#define L_HP (L_DM + 1024)
+#define L_DOUT (L_HP + 256)
+#define L_ST (L_DOUT + 16)
+#define L_SEL (L_ST + 32)
+#define L_TOTAL (L_SEL + 8)
+
+template <int A, int MODE, int NET>
+__device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
+  constexpr int O = NET ? 1 : 2 * A;
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, q = lane >> 4, w = tid >> 6;
+  const int tile = blockIdx.x;
+  const int g = c >> 2, n = c & 3;
+  const int graph = 4 * tile + g;
+  const bool gvalid = graph < ga.n_graphs;
+  const GnnNetOff off = gnn_net_off(A, NET);
+  const float* __restrict__ th = ga.theta;
+  if (MODE == GNN_ACT && NET == 0 && ga.bootstrap) return;   // bootstrap: critic only
+
+  // ---- locate this lane's graph (X [4][23]) and the selected node ----
+  const float* X;
+  int sel = 0;
+  int ridx = 0;
+  if constexpr (MODE == GNN_ACT) {
+    X = ga.x + (size_t)(gvalid ? graph : 0) * 92;
+  } else if constexpr (MODE == GNN_FWD) {
+    X = ga.x + (size_t)(gvalid ? graph : 0) * 92;
+    sel = gvalid ? ga.node[graph] : 0;
+  } else {
+    const UpdateArgs& U = ga.u;
+    const int e = ga.step / U.nb, b = ga.step - e * U.nb;
+    ridx = gvalid ? U.shuffle[U.perm[e * U.nb + b] * DDRL_MB + graph] : 0;
+    X = U.rec + (size_t)ridx * U.lay.stride + U.lay.obs;
+    sel = gvalid ? (int)X[92] : 0;
+  }
+  const float* xr = X + n * 23;
+  float fi[GNI];
+#pragma unroll
+  for (int k = 0; k < GNI; ++k) {
+    const int i = w + 4 * k;
+    fi[k] = i < GF ? xr[i] : 0.f;
+  }
+  const float qv = xr[GF + q];   // B operand of the hypernet MFMA: q_row[c][q]
+
+  // ---- weights of this wave into registers (read once per launch) ----
+  float we[GNI][4];
+  floatx4 be[GNI][4];
+#pragma unroll
+  for (int k = 0; k < GNI; ++k) {
+    const int i = w + 4 * k;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int j = i * 64 + 16 * t;
+      we[k][t] = i < GF ? th[off.wenc + q * GHE + j + c] : 0.f;
+      be[k][t] = i < GF ? *reinterpret_cast<const floatx4*>(th + off.benc + j + 4 * q) : splat4(0.f);
+    }
+  }
+  float wmf[4][4], wnf[4][4], wo[4][O];
+#pragma unroll
+  for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = 16 * fb + 4 * q + r;
+      wmf[fb][r] = th[off.wmsg + k * 64 + 16 * w + c];
+      wnf[fb][r] = th[off.wnode + k * 64 + 16 * w + c];
+    }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int o = 0; o < O; ++o) wo[r][o] = th[off.wout + (16 * w + 4 * q + r) * O + o];
+
+  // ---- hypernetwork + per-node encoding (partial over this wave's feature rows) ----
+  floatx4 hacc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) hacc[t] = splat4(0.f);
+#pragma unroll
+  for (int k = 0; k < GNI; ++k) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const floatx4 pre = mfma4(we[k][t], qv, be[k][t]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hacc[t][r] = fmaf(fi[k], tanh_fast(pre[r]), hacc[t][r]);
+    }
+  }
+  float* part = lds + L_PART;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) part[w * 1024 + (4 * t + r) * 64 + lane] = hacc[t][r];
+  __syncthreads();
+  float* himg = lds + L_H;
+  {
+    // wave w finalizes feature block t = w: h = tanh(sum of the four partials, fixed order)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = (4 * w + r) * 64 + lane;
+      const float s = ((part[o] + part[1024 + o]) + part[2048 + o]) + part[3072 + o];
+      himg[wbase(r) + 16 * w] = tanh_fast(s);
+    }
+  }
+  __syncthreads();
+  float h[4][4];
+#pragma unroll
+  for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) h[fb][r] = himg[wbase(r) + 16 * fb];
+
+  // ---- MPNN: msg and node for output block w ----
+  floatx4 msg = splat4(0.f), nod = splat4(0.f);
+#pragma unroll
+  for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      msg = mfma4(wmf[fb][r], h[fb][r], msg);
+      nod = mfma4(wnf[fb][r], h[fb][r], nod);
+    }
+  float y[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float m = 0.5f * (quad_next(msg[r]) + quad_prev(msg[r]));
+    y[r] = tanh_fast(nod[r] + m);
+  }
+  // ---- head: partial dot over this wave's 16 features, then across waves ----
+  float* hp = lds + L_HP;
+#pragma unroll
+  for (int o = 0; o < O; ++o) {
+    float acc = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc = fmaf(y[r], wo[r][o], acc);
+    acc = qsum(acc);
+    if (q == 0) hp[(w * 16 + c) * 4 + o] = acc;
+  }
+  __syncthreads();
+
+  if constexpr (MODE == GNN_ACT) {
+    if (tid < 16) {
+      const int cc = tid, gg = cc >> 2, nn = cc & 3, e = 4 * tile + gg;
+      if (e < ga.n_graphs) {
+        float out[O];
+#pragma unroll
+        for (int o = 0; o < O; ++o)
+          out[o] = (((hp[cc * 4 + o] + hp[(16 + cc) * 4 + o]) + hp[(32 + cc) * 4 + o]) +
+                    hp[(48 + cc) * 4 + o]) + th[off.bout + o];
+        const int C = 4 * ga.n_graphs;
+        const int row = e * 4 + nn;
+        if (NET == 1) {
+          if (ga.bootstrap) ga.last_v[row] = out[0];
+          else ga.rec[((size_t)ga.t * C + row) * ga.lay.stride + ga.lay.vf] = out[0];
+        } else {
+          float* rp = ga.rec + ((size_t)ga.t * C + row) * ga.lay.stride;
+          float logp = -0.5f * (float)(DDRL_LOG2PI * A);
+#pragma unroll
+          for (int j = 0; j < A; ++j) {
+            const float mu = out[j], ls = out[A + j];
+            const float sd = expf(ls);
+            const float a = mu + sd * ga.eps[((size_t)e * ga.n_agents + nn) * A + j];
+            const float z = (a - mu) / sd;
+            logp -= 0.5f * z * z;
+            logp -= ls;
+            rp[ga.lay.act + j] = a;
+            ga.actions[(size_t)e * 8 + ga.act_index[nn][j]] = fminf(fmaxf(a, -1.f), 1.f);
+          }
+#pragma unroll
+          for (int o = 0; o < O; ++o) rp[ga.lay.logit + o] = out[o];
+          rp[ga.lay.logp] = logp;
+        }
+      }
+    }
+    if (NET == 0 && !ga.bootstrap) {
+      // graph observation + node index into the 16 records of the tile
+      const int C = 4 * ga.n_graphs;
+      for (int idx = tid; idx < 16 * 93; idx += 256) {
+        const int rr = idx / 93, f = idx - rr * 93, e = 4 * tile + (rr >> 2);
+        if (e >= ga.n_graphs) continue;
+        const float v = f < 92 ? ga.x[(size_t)e * 92 + f] : (float)(rr & 3);
+        ga.rec[((size_t)ga.t * C + e * 4 + (rr & 3)) * ga.lay.stride + ga.lay.obs + f] = v;
+      }
+    }
+    return;
+  }
+  if constexpr (MODE == GNN_FWD) {
+    if (tid < 16) {
+      const int cc = tid, gg = cc >> 2, nn = cc & 3, r = 4 * tile + gg;
+      if (r < ga.n_graphs && nn == ga.node[r]) {
+#pragma unroll
+        for (int o = 0; o < O; ++o) {
+          const float v = (((hp[cc * 4 + o] + hp[(16 + cc) * 4 + o]) + hp[(32 + cc) * 4 + o]) +
+                           hp[(48 + cc) * 4 + o]) + th[off.bout + o];
+          if (NET == 0) ga.logits[(size_t)r * O + o] = v;
+          else ga.values[r] = v;
+        }
+      }
+    }
+    return;
+  }
+
+  // ===================== GNN_GRAD: loss + backward + partial gradients ==================
+  const UpdateArgs& U = ga.u;
+  const UpdateHyper& H = ga.h;
+  float* dsh = lds + L_DOUT;   // [4 graphs][4]
+  float* sts = lds + L_ST;     // [4 graphs][8]
+  if (tid < 16) {
+    const int cc = tid, gg = cc >> 2, nn = cc & 3;
+    if (nn == sel) {
+      const bool ok = gvalid;
+      float out[O], dout[O], st[5];
+#pragma unroll
+      for (int o = 0; o < O; ++o)
+        out[o] = (((hp[cc * 4 + o] + hp[(16 + cc) * 4 + o]) + hp[(32 + cc) * 4 + o]) +
+                  hp[(48 + cc) * 4 + o]) + th[off.bout + o];
+      const float* rp = U.rec + (size_t)ridx * U.lay.stride;
+      if constexpr (NET == 0) {
+        float act[A], ol[2 * A];
+#pragma unroll
+        for (int j = 0; j < A; ++j) act[j] = rp[U.lay.act + j];
+#pragma unroll
+        for (int j = 0; j < 2 * A; ++j) ol[j] = rp[U.lay.logit + j];
+        const float adv = (rp[U.lay.adv] - U.adv_norm[0]) / U.adv_norm[1];
+        policy_loss_row<A>(out, act, ol, rp[U.lay.logp], adv, U.kl_coeff, 1.f - H.clip, 1.f + H.clip,
+                           H.ent_coeff, ga.inv_n, ok, dout, st);
+        st[3] = st[4] = 0.f;
+      } else {
+        value_loss_row(out[0], rp[U.lay.vf], rp[U.lay.vt], H, ga.inv_n, ok, dout, st);
+      }
+#pragma unroll
+      for (int o = 0; o < O; ++o) dsh[gg * 4 + o] = dout[o];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) sts[gg * 8 + k] = st[k];
+    }
+  }
+  __syncthreads();
+  // per-tile statistics partial (fixed order over the 4 graphs)
+  if (tid < 5) {
+    float s = 0.f;
+    for (int gg = 0; gg < 4; ++gg) s += (4 * tile + gg < ga.n_graphs) ? sts[gg * 8 + tid] : 0.f;
+    ga.statp[(NET * (DDRL_MB / 4) + tile) * 8 + tid] = s;
+  }
+  float* P = ga.part + (size_t)tile * ga.part_stride;
+  const bool is_sel = n == sel;
+  float ds[O];
+#pragma unroll
+  for (int o = 0; o < O; ++o) ds[o] = is_sel ? dsh[g * 4 + o] : 0.f;
+  // dWout / dbout
+  if constexpr (O == 4) {
+    float v[16];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int o = 0; o < 4; ++o) v[4 * r + o] = y[r] * ds[o];
+    const float s = row16_transpose_sum(v);
+    P[off.wout + (16 * w + 4 * q + (c >> 2)) * 4 + (c & 3)] = s;
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = row16_sum(y[r] * ds[0]);
+      if (c == 0) P[off.wout + (16 * w + 4 * q + r) * O] = v;
+    }
+  }
+  if (tid < O) {
+    float s = 0.f;
+    for (int gg = 0; gg < 4; ++gg) s += dsh[gg * 4 + tid] * (4 * tile + gg < ga.n_graphs ? 1.f : 0.f);
+    P[off.bout + tid] = s;
+  }
+  // dy -> du = dy (1 - y^2) -> dm (ring mean transposed)
+  float du[4], dm[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float dy = 0.f;
+#pragma unroll
+    for (int o = 0; o < O; ++o) dy = fmaf(ds[o], wo[r][o], dy);
+    du[r] = dy * (1.f - y[r] * y[r]);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) dm[r] = 0.5f * (quad_next(du[r]) + quad_prev(du[r]));
+  float* duimg = lds + L_DU;
+  float* dmimg = lds + L_DM;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    duimg[wbase(r) + 16 * w] = du[r];
+    dmimg[wbase(r) + 16 * w] = dm[r];
+  }
+  // weights for dh: A[c][q] = W[16 w + c][16 fb + 4 q + r]
+  float wnb[4][4], wmb[4][4];
+#pragma unroll
+  for (int fb = 0; fb < 4; ++fb) {
+    const floatx4 a = *reinterpret_cast<const floatx4*>(th + off.wnode + (16 * w + c) * 64 + 16 * fb + 4 * q);
+    const floatx4 b = *reinterpret_cast<const floatx4*>(th + off.wmsg + (16 * w + c) * 64 + 16 * fb + 4 * q);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { wnb[fb][r] = a[r]; wmb[fb][r] = b[r]; }
+  }
+  __syncthreads();
+  // dh (block w) = Wnode . du^T + Wmsg . dm^T ;  dz = dh (1 - h^2)
+  floatx4 dh = splat4(0.f);
+#pragma unroll
+  for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      dh = mfma4(wnb[fb][r], duimg[wbase(r) + 16 * fb], dh);
+      dh = mfma4(wmb[fb][r], dmimg[wbase(r) + 16 * fb], dh);
+    }
+  // the hypernet partials are consumed: reuse PART for the dz exchange [block][r][lane]
+#pragma unroll
+  for (int r = 0; r < 4; ++r) part[(4 * w + r) * 64 + lane] = dh[r] * (1.f - h[w][r] * h[w][r]);
+  // dWnode, dWmsg: 32 tiles of 16x16 over the 16 rows, 8 per wave
+#pragma unroll 2
+  for (int k = 0; k < 8; ++k) {
+    const int id = w + 4 * k;            // 0..31
+    const int mat = id >> 4, kb = (id >> 2) & 3, ob = id & 3;
+    const floatx4 t = dw_tile<16>(himg, mat ? dmimg : duimg, kb, ob);
+    const int base = (mat ? off.wmsg : off.wnode) + 16 * ob + c;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) P[base + (16 * kb + 4 * q + r) * 64] = t[r];
+  }
+  __syncthreads();
+  float dz[4][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dz[t][r] = part[(4 * t + r) * 64 + lane];
+  float qa[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) qa[d] = xr[GF + d];
+  // hypernet backward: recompute W_n rows, dpre = f_i dz (1 - W^2); dWenc = q^T dpre,
+  // dbenc = sum of dpre, both reduced over the 16 rows of the DPP row.
+#pragma unroll
+  for (int k = 0; k < GNI; ++k) {
+    const int i = w + 4 * k;
+    if (i >= GF) break;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const floatx4 pre = mfma4(we[k][t], qv, be[k][t]);
+      float dp[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float wn = tanh_fast(pre[r]);
+        dp[r] = fi[k] * dz[t][r] * (1.f - wn * wn);
+      }
+      float v[16];
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[4 * d + r] = qa[d] * dp[r];
+      const float s = row16_transpose_sum(v);
+      const int j = i * 64 + 16 * t + 4 * q;
+      P[off.wenc + (c >> 2) * GHE + j + (c & 3)] = s;
+      float b[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) b[r] = row16_sum(dp[r]);
+      if (c < 4) P[off.benc + j + c] = c == 0 ? b[0] : c == 1 ? b[1] : c == 2 ? b[2] : b[3];
+    }
+  }
+}
+
+template <int A, int MODE>
+__global__ void __launch_bounds__(256) k_gnn(GnnArgs ga) {
+  __shared__ float lds[L_TOTAL];
+  if (blockIdx.y == 0) gnn_tile<A, MODE, 0>(ga, lds);
+  else gnn_tile<A, MODE, 1>(ga, lds);
+}
+
+// ---- reduction over tiles: grad[p] = sum_t part[t][p] (fixed order) + norm^2 partials ----
+__global__ void __launch_bounds__(256) k_gnn_reduce(GnnArgs ga, int ntiles, int n) {
+  __shared__ float red[4];
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  float s = 0.f;
+  if (p < n)
+    for (int t = 0; t < ntiles; ++t) s += ga.part[(size_t)t * ga.part_stride + p];
+  if (p < n) ga.grad[p] = s;
+  float ss = wave_sum(s * s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  if (threadIdx.x == 0) ga.normp[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+  if (blockIdx.x == 0 && threadIdx.x == 64) {
+    // loss statistics of the step: statp [tile][8] per net (actor block then critic block)
+    const UpdateArgs& U = ga.u;
+    ga.bp_cur[0] = U.beta_pow[0];
+    ga.bp_cur[1] = U.beta_pow[1];
+    if (U.stats) {
+      float sv[2][5];
+      for (int b = 0; b < 2; ++b)
+        for (int k = 0; k < 5; ++k) {
+          float a = 0.f;
+          for (int t = 0; t < ntiles; ++t) a += ga.statp[(b * DDRL_MB / 4 + t) * 8 + k];
+          sv[b][k] = a;
+        }
+      const float nr = (float)ga.n_graphs;
+      float* so = U.stats + (size_t)ga.step * 8;
+      so[1] = sv[0][0] / nr; so[3] = sv[0][1] / nr; so[4] = sv[0][2] / nr;
+      so[2] = sv[1][0] / nr;
+      const float vy = sv[1][2] / nr - (sv[1][1] / nr) * (sv[1][1] / nr);
+      const float vd = sv[1][4] / nr - (sv[1][3] / nr) * (sv[1][3] / nr);
+      so[5] = vy > 0.f ? fmaxf(-1.f, 1.f - vd / vy) : 0.f;
+    }
+  }
+}
+
+// ---- tf.clip_by_global_norm + tf1 Adam over all parameters of the policy ----
+__global__ void __launch_bounds__(256) k_gnn_adam(GnnArgs ga, int nred, int n) {
+  __shared__ float scale_s;
+  const UpdateArgs& U = ga.u;
+  const UpdateHyper& h = ga.h;
+  if (threadIdx.x == 0) {
+    float tot = 0.f;
+    for (int b = 0; b < nred; ++b) tot += ga.normp[b];
+    const float gn = sqrtf(tot);
+    scale_s = h.grad_clip * fminf(1.f / gn, 1.f / h.grad_clip);
+    if (blockIdx.x == 0) {
+      if (U.stats) {
+        U.stats[(size_t)ga.step * 8 + 6] = gn;
+        U.stats[(size_t)ga.step * 8 + 7] = scale_s;
+      }
+      U.beta_pow[0] = ga.bp_cur[0] * h.b1;
+      U.beta_pow[1] = ga.bp_cur[1] * h.b2;
+    }
+  }
+  __syncthreads();
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= n) return;
+  const float b1p = ga.bp_cur[0], b2p = ga.bp_cur[1];
+  const float alpha = h.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+  const float g = ga.grad[p] * scale_s;
+  float mi = U.m[p], vi = U.v[p];
+  mi = mi + (g - mi) * (1.f - h.b1);
+  vi = vi + (g * g - vi) * (1.f - h.b2);
+  U.m[p] = mi;
+  U.v[p] = vi;
+  U.theta[p] = U.theta[p] - (mi * alpha) / (sqrtf(vi) + h.eps);
+}
+
+int gnn_param_total(int A) { return gnn_net_off(A, 1).bout + 1; }
+
+static void check_a(int A) {
+  if (A != 2) {
+    fprintf(stderr, "ddrl: gnn kernels are built for act_dim 2 (got %d)\n", A);
+    abort();
+  }
+}
+
+void launch_act_gnn(hipStream_t s, const RouteArgs& ra, const ActArgs& aa) {
+  check_a(ra.A);
+  GnnArgs ga{};
+  ga.theta = aa.theta[0];
+  ga.n_graphs = ra.N;
+  ga.x = aa.stage[0];
+  ga.rec = aa.rec[0]; ga.lay = aa.lay[0]; ga.t = aa.t; ga.eps = aa.eps; ga.actions = aa.actions;
+  ga.n_agents = ra.n_agents; ga.bootstrap = aa.bootstrap; ga.last_v = aa.last_v[0];
+  for (int a = 0; a < 4; ++a)
+    for (int j = 0; j < 8; ++j) ga.act_index[a][j] = ra.pol[0].act_index[a][j];
+  hipLaunchKernelGGL((k_gnn<2, GNN_ACT>), dim3((ra.N + 3) / 4, 2), dim3(256), 0, s, ga);
+}
+
+void launch_forward_gnn(hipStream_t s, const ForwardArgs& fa) {
+  check_a(fa.A);
+  GnnArgs ga{};
+  ga.theta = fa.theta; ga.n_graphs = fa.n; ga.x = fa.x; ga.node = fa.node;
+  ga.logits = fa.logits; ga.values = fa.values;
+  hipLaunchKernelGGL((k_gnn<2, GNN_FWD>), dim3((fa.n + 3) / 4, 2), dim3(256), 0, s, ga);
+}
+
+void launch_step_gnn(hipStream_t s, const UpdateArgs& u, const UpdateHyper& h, int step, int nrows, float inv_n,
+                     const GnnScratch& sc) {
+  check_a(u.A);
+  GnnArgs ga{};
+  ga.theta = u.theta; ga.u = u; ga.h = h; ga.step = step; ga.n_graphs = nrows; ga.inv_n = inv_n;
+  ga.part = sc.part; ga.part_stride = sc.part_stride; ga.statp = sc.statp; ga.normp = sc.normp;
+  ga.bp_cur = sc.bp_cur; ga.grad = u.grad_out ? u.grad_out : sc.grad;
+  const int ntiles = (nrows + 3) / 4;
+  const int n = gnn_param_total(u.A);
+  // tiles of the critic write their statistics after the actor's: statp [2][32][8]
+  hipLaunchKernelGGL((k_gnn<2, GNN_GRAD>), dim3(ntiles, 2), dim3(256), 0, s, ga);
+  const int nred = (n + 255) / 256;
+  hipLaunchKernelGGL(k_gnn_reduce, dim3(nred), dim3(256), 0, s, ga, ntiles, n);
+  if (!u.grad_out) hipLaunchKernelGGL(k_gnn_adam, dim3(nred), dim3(256), 0, s, ga, nred, n);
+}

@@ -7,6 +7,9 @@
 #define DDRL_MAXAG 4      // agents per env
 #define DDRL_MAXD 48      // per-agent observation width
 #define DDRL_MAXFULL 48   // full observation width (43 / 44)
+#ifndef DDRL_MB
+#define DDRL_MB 128       // sgd_minibatch_size supported by the update kernels
+#endif
 
 // Record (one training row) layout, in floats.  Rows are time-major:
 //   row = t * C + c,  c = env * k + slot  (k agents of this policy per env).
@@ -105,7 +108,6 @@ struct UpdateHyper {
 // ua_dev: device array of h.P UpdateArgs (one persistent workgroup per entry)
 void launch_update_ffn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHyper& h, int nrows, float inv_n, int A, int d,
                        unsigned long long* xchg, int* err);
-void launch_update_gnn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHyper& h, int nrows, float inv_n, int A);
 // clip_by_global_norm + tf1 Adam on a flat (all-reduced) gradient vector
 void launch_apply_adam(hipStream_t s, const float* grad, int n, float* theta, float* m, float* v,
                        float* beta_pow, const UpdateHyper& h);
@@ -117,3 +119,27 @@ struct ForwardArgs {
 };
 void launch_forward_ffn(hipStream_t s, const ForwardArgs& fa);
 void launch_forward_gnn(hipStream_t s, const ForwardArgs& fa);
+
+// ---- GraphNet (gnn.hip): per-tile kernels, one minibatch step = grad / reduce / Adam ----
+struct GnnArgs {
+  const float* theta;
+  int n_graphs;                 // envs (act), rows (forward) or minibatch rows (grad)
+  const float* x;               // act: stage [N][4][23]; forward: [n][4][23]
+  const int32_t* node;          // forward: node of every row
+  // act
+  float* rec; RecLayout lay; int t; const float* eps; float* actions; int n_agents;
+  int act_index[4][8]; int bootstrap; float* last_v;
+  // forward
+  float* logits; float* values;
+  // grad
+  UpdateArgs u; UpdateHyper h; int step; float inv_n;
+  float* part; int part_stride;  // [tiles][n_params] partial gradients
+  float* statp;                  // [2 nets][32 tiles][8]
+  float* normp;                  // [reduce blocks] squared-norm partials
+  float* bp_cur;                 // [2] beta powers of the current step
+  float* grad;                   // reduced gradient (scratch or the DDP output)
+};
+struct GnnScratch { float* part; int part_stride; float* statp; float* normp; float* bp_cur; float* grad; };
+int gnn_param_total(int A);
+void launch_step_gnn(hipStream_t s, const UpdateArgs& u, const UpdateHyper& h, int step, int nrows, float inv_n,
+                     const GnnScratch& sc);

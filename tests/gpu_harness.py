@@ -148,12 +148,12 @@ def synthetic_inputs(rng, cfg, T):
     return obs, eps, fw, cfrc, done
 
 
-def run_rollout(ctx, cfg, inst, params, rng, filt, T):
+def run_rollout(ctx, cfg, inst, params, rng, filt, T, orc_cls=None):
     """Run the HIP rollout and the oracle on the same inputs; returns (oracle, inputs)."""
     import torch
     obs, eps, fw, cfrc, done = synthetic_inputs(rng, cfg, T)
     ctx.filter_set(*filt)
-    orc = OracleRollout(cfg, inst, params, filt)
+    orc = (orc_cls or OracleRollout)(cfg, inst, params, filt)
     dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
     actions = torch.zeros((cfg.n_envs, 8), dtype=torch.float32, device="cuda")
     acts_gpu = []
@@ -179,3 +179,62 @@ def run_rollout(ctx, cfg, inst, params, rng, filt, T):
     norms = orc.gae()
     torch.cuda.synchronize()
     return orc, norms, np.stack(acts_gpu), np.stack(acts_orc)
+
+
+# --------------------------------------------------------------------------------------
+# GraphNet ("gnn", DecentralShared_Graph): one shared leg policy, 4 rows per env (node n
+# = agent n), record obs field = X [4][23] flattened + node index.
+# --------------------------------------------------------------------------------------
+GNN_ENV = "QuantrupedMultiEnv_DecentralShared_Graph"
+
+
+def init_gnn_params(ctx, seed, head_scale=1.0, A=2):
+    rng = np.random.default_rng(seed)
+    p = O.gnn_init(rng, 2 * A)
+    for net in ("actor/", "critic/"):
+        p[net + "linear_out/kernel"] *= head_scale
+        p[net + "state_enc/bias"] += (rng.normal(size=p[net + "state_enc/bias"].shape) * 0.2).astype(np.float32)
+    p["actor/linear_out/bias"] += np.concatenate([np.zeros(A), -0.5 * np.ones(A)]).astype(np.float32)
+    ctx.params_set(0, O.pack(p, O.gnn_param_shapes(2 * A)))
+    return p
+
+
+class GnnOracleRollout(OracleRollout):
+    def __init__(self, cfg, inst, params, filt):
+        super().__init__(cfg, inst, params[0] if isinstance(params, list) else params, filt)
+        self.params = [params] if not isinstance(params, list) else params
+        T, N_ = cfg.frag_len, cfg.n_envs
+        self.rec[0]["obs"] = np.zeros((T, N_ * 4, 93), np.float32)
+        self.node_tables = [inst.obs_indices[a] for a in self.agents]
+
+    def observe(self, obs):
+        normed = O.mean_std_filter(obs, self.rs, update=True, clip=self.cfg.filter_clip)
+        X = np.stack([O.graph_observation(obs[e].astype(np.float64), normed[e], self.node_tables)
+                      for e in range(obs.shape[0])]).astype(np.float32)
+        self.stage = [X]
+
+    def _forward_all(self):
+        X = self.stage[0]
+        N_ = X.shape[0]
+        Xr = np.repeat(X, 4, axis=0)                     # row c = e * 4 + n
+        node = np.tile(np.arange(4), N_)
+        logits, value, _ = O.gnn_forward(self.params[0], Xr, node)
+        return Xr, node, logits, value
+
+    def act(self, t, eps):
+        cfg = self.cfg
+        A = cfg.act_dim
+        Xr, node, logits, value = self._forward_all()
+        a = O.dg_sample(logits, eps.reshape(-1, A))
+        r = self.rec[0]
+        r["obs"][t, :, :92] = Xr.reshape(-1, 92)
+        r["obs"][t, :, 92] = node
+        r["act"][t], r["logits"][t] = a, logits
+        r["logp"][t], r["vf"][t] = O.dg_logp(logits, a), value
+        actions = np.zeros((cfg.n_envs, 8), np.float32)
+        for s, name in enumerate(self.agents):
+            actions[:, self.inst.action_indices[name]] = np.clip(a.reshape(-1, 4, A)[:, s], -1, 1)
+        return actions
+
+    def bootstrap(self):
+        self.last_v = [self._forward_all()[3]]
