@@ -51,6 +51,7 @@ struct ddrl_ctx {
   Policy pol[DDRL_MAXP];
   RouteArgs route{};
   double *f_n = nullptr, *f_M = nullptr, *f_S = nullptr, *f_normc = nullptr;
+  double *f_dn = nullptr, *f_dM = nullptr, *f_dS = nullptr;   // pushes since the last sync
   uint8_t* done_tn = nullptr;
   float** stage_tab = nullptr;    // device array of per-policy stage pointers
   int32_t* zero_perm = nullptr;
@@ -169,7 +170,7 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
          dalloc(c, &P.v, P.n_params) || dalloc(c, &P.beta_pow, 2) || dalloc(c, &P.grad, P.n_params) ||
          dalloc(c, &P.rec, (size_t)P.R * P.lay.stride) || dalloc(c, &P.stage, stage_n) ||
          dalloc(c, &P.last_v, P.C) || dalloc(c, &P.adv_norm, 2) ||
-         dalloc(c, &P.partials, 2 * (size_t)((P.C + 255) / 256)) ||
+         dalloc(c, &P.partials, 2 * (size_t)((P.C + 255) / 256) + 4) ||
          dalloc(c, &P.stats, (size_t)g.num_sgd_iter * P.nb * 8);
     if (!rc) {
       float bp[2] = {g.adam_beta1, g.adam_beta2};
@@ -179,7 +180,8 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
     }
   }
   rc = rc || dalloc(c, &c->f_n, 1) || dalloc(c, &c->f_M, DDRL_MAXFULL) || dalloc(c, &c->f_S, DDRL_MAXFULL) ||
-       dalloc(c, &c->f_normc, 2 * DDRL_MAXFULL) || dalloc(c, &c->done_tn, (size_t)T * N) ||
+       dalloc(c, &c->f_normc, 2 * DDRL_MAXFULL) || dalloc(c, &c->f_dn, 1) ||
+       dalloc(c, &c->f_dM, DDRL_MAXFULL) || dalloc(c, &c->f_dS, DDRL_MAXFULL) || dalloc(c, &c->done_tn, (size_t)T * N) ||
        dalloc(c, &c->stage_tab, DDRL_MAXP) || dalloc(c, &c->zero_perm, 4) ||
        dalloc(c, &c->d_uargs, DDRL_MAXP) || dalloc(c, &c->xchg, 4 * DDRL_MAXP) || dalloc(c, &c->err, 1) ||
        dalloc(c, &c->h_obs, (size_t)N * g.obs_full_dim) ||
@@ -318,12 +320,40 @@ int ddrl_filter_get(ddrl_ctx* c, double* n, double* M, double* S) {
   return 0;
 }
 
+int ddrl_filter_delta_get(ddrl_ctx* c, double* n, double* M, double* S) {
+  CHK_CTX(c);
+  const int D = c->cfg.obs_full_dim;
+  HIPCHK(hipMemcpyAsync(n, c->f_dn, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(M, c->f_dM, D * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(S, c->f_dS, D * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int ddrl_filter_delta_reset(ddrl_ctx* c) {
+  CHK_CTX(c);
+  HIPCHK(hipMemsetAsync(c->f_dn, 0, 8, c->stream));
+  HIPCHK(hipMemsetAsync(c->f_dM, 0, DDRL_MAXFULL * 8, c->stream));
+  HIPCHK(hipMemsetAsync(c->f_dS, 0, DDRL_MAXFULL * 8, c->stream));
+  return 0;
+}
+
+int ddrl_adv_sums_get(ddrl_ctx* c, int pid, double* host3) {
+  CHK_CTX(c);
+  if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
+  const Policy& P = c->pol[pid];
+  const size_t nblocks = (P.C + 255) / 256;
+  HIPCHK(hipMemcpyAsync(host3, P.partials + 2 * nblocks, 3 * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
 int ddrl_observe(ddrl_ctx* c, const float* obs) {
   CHK_CTX(c);
   if (!obs) return fail("null observation buffer");
   const ddrl_cfg& g = c->cfg;
   launch_filter_push(c->stream, obs, g.n_envs, g.obs_full_dim, c->f_n, c->f_M, c->f_S, c->f_normc,
-                     g.filter_update, g.filter_enabled);
+                     g.filter_update, g.filter_enabled, c->f_dn, c->f_dM, c->f_dS);
   if (g.model_kind == DDRL_MODEL_FFN)
     launch_observe_ffn(c->stream, c->route, obs, c->f_normc, g.filter_enabled ? g.filter_clip : 0.f,
                        c->stage_tab);
@@ -492,13 +522,17 @@ int ddrl_ppo_stats(ddrl_ctx* c, int pid, float* host, size_t n_steps) {
   return 0;
 }
 
-int ddrl_ppo_grad(ddrl_ctx* c, int pid, const int32_t* rows, int n_rows, float kl, float* grad) {
+int ddrl_ppo_grad(ddrl_ctx* c, int pid, const int32_t* rows, int n_rows, float kl, float* grad,
+                  int stats_step) {
   CHK_CTX(c);
   if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
   if (n_rows < 1 || n_rows > 128) return fail("n_rows must be in [1, 128]");
   if (!rows || !grad) return fail("null rows/grad");
+  if (stats_step >= c->cfg.num_sgd_iter * c->pol[pid].nb) return fail("stats_step beyond the stats buffer");
   UpdateArgs u = make_update(c, pid, rows, c->zero_perm, kl);
-  u.nb = 1; u.n_epochs = 1; u.max_steps = 1; u.step0 = 0; u.grad_out = grad; u.stats = nullptr;
+  u.nb = 1; u.n_epochs = 1; u.max_steps = 1; u.step0 = 0; u.grad_out = grad;
+  u.stats = stats_step >= 0 ? c->pol[pid].stats + (size_t)stats_step * 8 : nullptr;
+  c->kl_last[pid] = kl;
   UpdateHyper h = make_hyper(c, 1);
   HIPCHK(hipMemcpyAsync(c->d_uargs, &u, sizeof(UpdateArgs), hipMemcpyHostToDevice, c->stream));
   if (c->cfg.model_kind == DDRL_MODEL_FFN)

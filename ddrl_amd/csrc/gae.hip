@@ -64,6 +64,9 @@ __global__ void k_gae_finalize(GaeArgs g, int nblocks) {
     s2 += g.partials[2 * b + 1];
   }
   const double n = (double)g.C * (double)g.T;
+  g.partials[2 * nblocks] = s1;        // for a cross-rank StandardizeFields
+  g.partials[2 * nblocks + 1] = s2;
+  g.partials[2 * nblocks + 2] = n;
   const double mean = s1 / n;
   double var = s2 / n - mean * mean;
   if (var < 0.0) var = 0.0;

@@ -34,8 +34,10 @@ struct RouteArgs {
 };
 
 // ---- filter / observe (rollout.hip) ----
+// dn / dM / dS: a second running stat of the pushes since the last cross-rank filter sync
 void launch_filter_push(hipStream_t s, const float* obs, int N, int D, double* n_run, double* M,
-                        double* S, double* normc, int update, int enabled);
+                        double* S, double* normc, int update, int enabled, double* dn, double* dM,
+                        double* dS);
 void launch_observe_ffn(hipStream_t s, const RouteArgs& ra, const float* obs, const double* normc,
                         float clip, float* const* stage);
 void launch_observe_gnn(hipStream_t s, const RouteArgs& ra, const float* obs, const double* normc,
@@ -81,7 +83,7 @@ struct GaeArgs {
   float* rec; RecLayout lay; int C, T, N, k;
   const float* last_v; const uint8_t* done_tn;
   double gamma, lambda_;
-  double* partials;   // [nblocks][2]
+  double* partials;   // [nblocks][2] + totals {sum adv, sum adv^2, count} after the blocks
   float* adv_norm;    // [2]: mean, max(1e-4, std)
 };
 void launch_gae(hipStream_t s, const GaeArgs& g);

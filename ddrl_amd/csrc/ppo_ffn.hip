@@ -110,6 +110,26 @@ __device__ __forceinline__ void load_row(const UpdateArgs& U, const int* ridx, c
   }
 }
 
+// Per-step learner statistics from the per-wave partial sums red[w * 8 + k]: policy
+// workgroup -> policy_loss, kl, entropy; value workgroup -> vf_loss, vf_explained_var.
+template <bool POL, int NSTAT>
+__device__ __forceinline__ void write_stats(float* so, const float* red, float n) {
+  float sv[NSTAT];
+#pragma unroll
+  for (int k = 0; k < NSTAT; ++k) {
+    sv[k] = 0.f;
+    for (int i = 0; i < NW; ++i) sv[k] += red[i * 8 + k];
+  }
+  if constexpr (POL) {
+    so[1] = sv[0] / n; so[3] = sv[1] / n; so[4] = sv[2] / n;
+  } else {
+    so[2] = sv[0] / n;
+    const float vy = sv[2] / n - (sv[1] / n) * (sv[1] / n);
+    const float vd = sv[4] / n - (sv[3] / n) * (sv[3] / n);
+    so[5] = vy > 0.f ? fmaxf(-1.f, 1.f - vd / vy) : 0.f;
+  }
+}
+
 __device__ __forceinline__ int row_index(const UpdateArgs& U, int step, int row_l, bool ok) {
   if (!ok) return 0;
   const int e = step / U.nb, b = step - e * U.nb;
@@ -371,6 +391,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
           U.grad_out[pidx] = gs[k];
         }
       }
+      if (U.stats && tid == 64) write_stats<POL, NSTAT>(U.stats + (size_t)step * 8, red, (float)ub.nrows);
       return;
     }
 
@@ -406,23 +427,9 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     __syncthreads();                                     // #5
     STAMP(8);
     if (U.stats && tid == 64) {   // off the critical path: wave 1, after the exchange
-      float sv[NSTAT];
-#pragma unroll
-      for (int k = 0; k < NSTAT; ++k) {
-        sv[k] = 0.f;
-        for (int i = 0; i < NW; ++i) sv[k] += red[i * 8 + k];
-      }
-      const float n = (float)ub.nrows;
-      float* so = U.stats + (size_t)step * 8;
-      if constexpr (POL) {
-        so[1] = sv[0] / n; so[3] = sv[1] / n; so[4] = sv[2] / n;
-        so[6] = red[80]; so[7] = red[81];
-      } else {
-        so[2] = sv[0] / n;
-        const float vy = sv[2] / n - (sv[1] / n) * (sv[1] / n);
-        const float vd = sv[4] / n - (sv[3] / n) * (sv[3] / n);
-        so[5] = vy > 0.f ? fmaxf(-1.f, 1.f - vd / vy) : 0.f;
-      }
+      write_stats<POL, NSTAT>(U.stats + (size_t)step * 8, red, (float)ub.nrows);
+      U.stats[(size_t)step * 8 + 6] = red[80];
+      U.stats[(size_t)step * 8 + 7] = red[81];
     }
     const float scale = red[81];
     const float alpha = H.lr * sqrtf(1.f - b2p) / (1.f - b1p);

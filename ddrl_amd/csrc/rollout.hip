@@ -19,7 +19,8 @@
 // ------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_filter_push(const float* __restrict__ obs, int N, int D,
                                                      double* n_run, double* M, double* S,
-                                                     double* normc, int update, int enabled) {
+                                                     double* normc, int update, int enabled,
+                                                     double* dn, double* dM, double* dS) {
   const int j = blockIdx.x;
   __shared__ double red[4];
   __shared__ double sh_mean;
@@ -56,6 +57,10 @@ __global__ void __launch_bounds__(256) k_filter_push(const float* __restrict__ o
       n1 = n;
       M[j] = Mj;
       S[j] = Sj;
+      // the same batch merged into the delta buffer (pushes since the last filter sync)
+      const double d1 = dn[0], dd = d1 + n2, ddl = dM[j] - mean_b;
+      dM[j] = (d1 * dM[j] + n2 * mean_b) / dd;
+      dS[j] = dS[j] + s_b + ddl * ddl * d1 * n2 / dd;
     }
     const double var = n1 > 1.0 ? Sj / (n1 - 1.0) : Mj * Mj;
     normc[2 * j] = enabled ? Mj : 0.0;
@@ -63,13 +68,17 @@ __global__ void __launch_bounds__(256) k_filter_push(const float* __restrict__ o
   }
 }
 
-__global__ void k_filter_count(double* n_run, int N) { n_run[0] += (double)N; }
+__global__ void k_filter_count(double* n_run, double* dn, int N) {
+  n_run[0] += (double)N;
+  dn[0] += (double)N;
+}
 
 void launch_filter_push(hipStream_t s, const float* obs, int N, int D, double* n_run, double* M,
-                        double* S, double* normc, int update, int enabled) {
+                        double* S, double* normc, int update, int enabled, double* dn, double* dM,
+                        double* dS) {
   hipLaunchKernelGGL(k_filter_push, dim3(D), dim3(256), 0, s, obs, N, D, n_run, M, S, normc,
-                     update, enabled);
-  if (enabled && update) hipLaunchKernelGGL(k_filter_count, dim3(1), dim3(1), 0, s, n_run, N);
+                     update, enabled, dn, dM, dS);
+  if (enabled && update) hipLaunchKernelGGL(k_filter_count, dim3(1), dim3(1), 0, s, n_run, dn, N);
 }
 
 __device__ __forceinline__ float norm_obs(float x, const double* normc, int idx, float clip) {

@@ -1,0 +1,151 @@
+"""Data-parallel learner for the shared-policy configurations (C4
+SharedDecentral, C5 DecentralShared_Graph).  One process per GPU, torch.distributed over
+RCCL ("nccl") on the GPU box or gloo for the CPU tests.
+
+Per iteration (RLlib semantics restated for G ranks that each own N / G envs):
+  * rollout on the rank's own envs with its own MeanStdFilter (like an RLlib worker);
+  * synchronize_filters (P_Local:160): every rank's pushes since the last sync (the filter
+    "buffer", `ddrl_filter_delta_get`) are all-gathered and merged into the synced filter
+    with RunningStat.update in rank order -- identical on every rank;
+  * StandardizeFields over the union batch: all-reduce of fp64 (sum adv, sum adv^2, n);
+  * minibatch SGD: per step every rank computes the gradient of its share of the
+    minibatch (`ddrl_ppo_grad`, scaled by 1 / sgd_minibatch_size), one all-reduce(sum)
+    of the flat gradient, then clip_by_global_norm + Adam locally (`ddrl_ppo_apply`),
+    identical on every rank;
+      mode "split": the global minibatch of 128 rows is 128 / G rows per rank -- the
+                    sum of the rank gradients IS the single-process minibatch gradient
+                    (the parity mode);
+      mode "local": every rank contributes 128 rows (global minibatch 128 G, gradient
+                    averaged over ranks), G times fewer sequential steps per epoch;
+  * update_kl from the all-reduced mean KL of the last epoch.
+Independent-policy configurations (Local, C3) need none of this: every rank is a replica.
+
+The learner drives a backend with grad / apply / stats (`HipBackend` wraps the C-ABI
+context); the collectives go through torch.distributed.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def merge_running_stats(base, deltas):
+    """RunningStat.update (Chan et al.) of every delta (n, M, S) into base, in order."""
+    n, M, S = float(base[0]), np.array(base[1], np.float64), np.array(base[2], np.float64)
+    for dn, dM, dS in deltas:
+        dn = float(dn)
+        if dn == 0:
+            continue
+        tot = n + dn
+        delta = M - np.asarray(dM, np.float64)
+        M = (n * M + dn * np.asarray(dM, np.float64)) / tot
+        S = S + np.asarray(dS, np.float64) + delta * delta * n * dn / tot
+        n = tot
+    return n, M, S
+
+
+def standardize_constants(sums):
+    """(mean, max(1e-4, std)) from fp64 (sum, sum of squares, count) exactly as the GAE
+    finalize kernel computes them (population std, fp32 results)."""
+    s1, s2, n = (float(v) for v in sums)
+    mean = s1 / n
+    var = max(s2 / n - mean * mean, 0.0)
+    return np.float32(mean), max(np.float32(1e-4), np.float32(np.sqrt(var)))
+
+
+class Comm:
+    """torch.distributed helpers on numpy arrays (tensors live on `device`: cuda for RCCL,
+    cpu for gloo)."""
+
+    def __init__(self, device="cpu", group=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.group = torch, dist, group
+        self.device = device
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+
+    def all_reduce_np(self, arr, op="sum"):
+        t = self.torch.as_tensor(np.ascontiguousarray(arr)).to(self.device)
+        self.dist.all_reduce(t, op=getattr(self.dist.ReduceOp, op.upper()), group=self.group)
+        return t.cpu().numpy()
+
+    def all_gather_np(self, arr):
+        t = self.torch.as_tensor(np.ascontiguousarray(arr)).to(self.device)
+        out = [self.torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t, group=self.group)
+        return [o.cpu().numpy() for o in out]
+
+    def all_reduce_(self, tensor):
+        if self.world > 1:
+            self.dist.all_reduce(tensor, group=self.group)
+
+
+def sync_filters(comm, base, delta):
+    """All-gather every rank's filter delta and merge them into `base` in rank order."""
+    D = len(delta[1])
+    packed = np.concatenate([[delta[0]], delta[1], delta[2]]).astype(np.float64)
+    parts = comm.all_gather_np(packed)
+    deltas = [(p[0], p[1:1 + D], p[1 + D:1 + 2 * D]) for p in parts]
+    return merge_running_stats(base, deltas)
+
+
+def sync_standardize(comm, sums):
+    """Global StandardizeFields constants from every rank's fp64 advantage sums."""
+    return standardize_constants(comm.all_reduce_np(np.asarray(sums, np.float64)))
+
+
+class HipBackend:
+    """The C-ABI context as a learner backend."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    def grad(self, pid, rows, n_rows, kl, grad, stats_step):
+        self.ctx.ppo_grad(pid, rows, n_rows, kl, grad, stats_step)
+
+    def apply(self, pid, grad):
+        self.ctx.ppo_apply(pid, grad)
+
+    def stats(self, pid, n):
+        return self.ctx.ppo_stats(pid, n)
+
+
+class DataParallelLearner:
+    def __init__(self, backend, comm, pid=0, minibatch=128, mode="split"):
+        if mode not in ("split", "local"):
+            raise ValueError("mode must be 'split' or 'local'")
+        if mode == "split" and minibatch % comm.world:
+            raise ValueError("split mode needs sgd_minibatch_size divisible by the world size")
+        self.backend, self.comm, self.pid, self.mode = backend, comm, pid, mode
+        self.rows_per_rank = minibatch // comm.world if mode == "split" else minibatch
+        self.grad_scale = 1.0 if mode == "split" else 1.0 / comm.world
+
+    def n_minibatches(self, rows_local):
+        """Steps per epoch: every rank must run the same number (the smallest shard wins)."""
+        nb = max(1, rows_local // self.rows_per_rank)
+        return int(self.comm.all_reduce_np(np.array([nb], np.int64), op="min")[0])
+
+    def schedule(self, rng, rows_local, epochs):
+        nb = self.n_minibatches(rows_local)
+        shuffle = rng.permutation(rows_local).astype(np.int32)
+        perms = np.stack([rng.permutation(nb) for _ in range(epochs)]).astype(np.int32)
+        return shuffle, perms
+
+    def learn(self, shuffle, perms, kl_coeff, grad):
+        """shuffle: rank-local row permutation (device tensor for the HIP backend),
+        perms: host int array [epochs][nb], grad: flat gradient buffer (device tensor).
+        Returns the all-reduced mean KL of the last epoch."""
+        E, nb = perms.shape
+        m = self.rows_per_rank
+        for e in range(E):
+            last = e == E - 1
+            for b in range(nb):
+                s = int(perms[e, b]) * m
+                self.backend.grad(self.pid, shuffle[s:s + m], m, kl_coeff, grad, b if last else -1)
+                self.comm.all_reduce_(grad)
+                if self.grad_scale != 1.0:
+                    grad.mul_(self.grad_scale)
+                self.backend.apply(self.pid, grad)
+        st = self.backend.stats(self.pid, nb)
+        kl_local = float(np.mean(st[:, 3].astype(np.float64)))
+        return float(self.comm.all_reduce_np(np.array([kl_local]))[0]) / self.comm.world

@@ -57,6 +57,9 @@ _SIGS = {
     "ddrl_adam_get": ([VP, C.c_int, VP, VP, C.c_size_t, C.POINTER(f32), C.POINTER(f32)], C.c_int),
     "ddrl_filter_set": ([VP, C.c_double, VP, VP], C.c_int),
     "ddrl_filter_get": ([VP, C.POINTER(C.c_double), VP, VP], C.c_int),
+    "ddrl_filter_delta_get": ([VP, C.POINTER(C.c_double), VP, VP], C.c_int),
+    "ddrl_filter_delta_reset": ([VP], C.c_int),
+    "ddrl_adv_sums_get": ([VP, C.c_int, VP], C.c_int),
     "ddrl_observe": ([VP, VP], C.c_int),
     "ddrl_act": ([VP, C.c_int, VP, VP], C.c_int),
     "ddrl_reward": ([VP, C.c_int, VP, VP, VP, VP], C.c_int),
@@ -65,7 +68,7 @@ _SIGS = {
     "ddrl_gae": ([VP], C.c_int),
     "ddrl_ppo_update": ([VP, C.c_int, C.POINTER(VP), C.POINTER(VP), C.POINTER(f32), C.c_int], C.c_int),
     "ddrl_ppo_stats": ([VP, C.c_int, VP, C.c_size_t], C.c_int),
-    "ddrl_ppo_grad": ([VP, C.c_int, VP, C.c_int, f32, VP], C.c_int),
+    "ddrl_ppo_grad": ([VP, C.c_int, VP, C.c_int, f32, VP, C.c_int], C.c_int),
     "ddrl_ppo_apply": ([VP, C.c_int, VP], C.c_int),
     "ddrl_policy_forward": ([VP, C.c_int, VP, VP, C.c_int, VP, VP], C.c_int),
     "ddrl_device_buffers": ([VP, C.c_int, C.POINTER(VP), C.POINTER(VP), C.POINTER(VP), C.POINTER(VP)], C.c_int),
@@ -200,6 +203,23 @@ class Context:
         _ck(self.lib.ddrl_filter_get(self.h, C.byref(n), M.ctypes.data, S.ctypes.data))
         return n.value, M, S
 
+    def filter_delta_get(self):
+        """Pushes since the last filter_delta_reset as (n, M, S)."""
+        D = self.cfg.obs_full_dim
+        n = C.c_double()
+        M, S = np.empty(D), np.empty(D)
+        _ck(self.lib.ddrl_filter_delta_get(self.h, C.byref(n), M.ctypes.data, S.ctypes.data))
+        return n.value, M, S
+
+    def filter_delta_reset(self):
+        _ck(self.lib.ddrl_filter_delta_reset(self.h))
+
+    def adv_sums_get(self, pid):
+        """fp64 (sum adv, sum adv^2, count) of the last gae() for policy pid."""
+        a = np.empty(3, np.float64)
+        _ck(self.lib.ddrl_adv_sums_get(self.h, pid, a.ctypes.data))
+        return a
+
     def records_get(self, pid):
         lay = self.layout[pid]
         a = np.empty((self.cfg.frag_len * lay["C"], lay["stride"]), np.float32)
@@ -259,8 +279,9 @@ class Context:
         _ck(self.lib.ddrl_ppo_stats(self.h, pid, a.ctypes.data, n_steps))
         return a
 
-    def ppo_grad(self, pid, rows_dev, n_rows, kl_coeff, grad_dev):
-        _ck(self.lib.ddrl_ppo_grad(self.h, pid, _ptr(rows_dev), n_rows, kl_coeff, _ptr(grad_dev)))
+    def ppo_grad(self, pid, rows_dev, n_rows, kl_coeff, grad_dev, stats_step=-1):
+        _ck(self.lib.ddrl_ppo_grad(self.h, pid, _ptr(rows_dev), n_rows, kl_coeff, _ptr(grad_dev),
+                                   stats_step))
 
     def ppo_apply(self, pid, grad_dev):
         _ck(self.lib.ddrl_ppo_apply(self.h, pid, _ptr(grad_dev)))

@@ -44,10 +44,17 @@ class PPOTrainer:
     """
 
     def __init__(self, config, n_envs=None, device=0, env_backend=None, seed=0, stream=None):
+        """Multi-process use: initialize torch.distributed first (one process per GPU).
+        Shared-policy envs then train data-parallel (config "parallel": "ddp", the default
+        for one policy; "ddp_mode": "split" | "local", see ddrl_amd.ddp); multi-policy envs
+        run as independent replicas ("parallel": "replicas")."""
         import torch
+        import torch.distributed as dist
         self.torch = torch
         self.config = {**PPO_DEFAULTS, **config}
         c = self.config
+        self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        self.rank = dist.get_rank() if self.world > 1 else 0
         env = c["env"]
         self.n_envs = int(n_envs or c.get("num_envs", c.get("num_workers", 2) * c.get("num_envs_per_worker", 4)))
         self.T = int(c["rollout_fragment_length"])
@@ -58,7 +65,8 @@ class PPOTrainer:
         self.ctx = N.Context(self.cfg, device, self.stream.cuda_stream)
         self.policy_ids = list(type(self.env).policy_names)
         P = self.cfg.n_policies
-        self.rng = np.random.default_rng(seed)
+        self.rng = np.random.default_rng(seed)              # weights: identical on every rank
+        self.sched_rng = np.random.default_rng(seed + 7919 * (self.rank + 1))
         for p in range(P):
             if self.cfg.model_kind == N.MODEL_FFN:
                 self.ctx.params_set(p, glorot_ffn_flat(self.rng, self.cfg.obs_dim[p], self.cfg.act_dim))
@@ -75,6 +83,15 @@ class PPOTrainer:
         self.noise_gen.manual_seed(seed + 1)
         self.timesteps_total = 0
         self.iteration = 0
+        self.parallel = c.get("parallel") or ("ddp" if self.world > 1 and P == 1 else "replicas")
+        if self.parallel == "ddp":
+            from .ddp import Comm, DataParallelLearner, HipBackend
+            self.comm = Comm(self.device if dist.get_backend() == "nccl" else "cpu")
+            self.learner = DataParallelLearner(HipBackend(self.ctx), self.comm, 0, self.cfg.sgd_minibatch_size,
+                                               c.get("ddp_mode", "split"))
+            self.filter_base = self.ctx.filter_get()
+            self.ctx.filter_delta_reset()
+            self.grad = torch.zeros(self.ctx.n_params[0], dtype=torch.float32, device=self.device)
         self.ctx.observe(self.backend.reset())
 
     # -- one iteration ---------------------------------------------------------------
@@ -89,17 +106,43 @@ class PPOTrainer:
             self.ctx.observe(obs)
         self.ctx.bootstrap()
         self.ctx.gae()
+        if self.parallel == "ddp":
+            from .ddp import sync_filters, sync_standardize
+            merged = sync_filters(self.comm, self.filter_base, self.ctx.filter_delta_get())
+            self.ctx.filter_set(*merged)
+            self.ctx.filter_delta_reset()
+            self.filter_base = merged
+            for p in range(self.cfg.n_policies):
+                self.ctx.adv_norm_set(p, *sync_standardize(self.comm, self.ctx.adv_sums_get(p)))
 
     def _schedule(self, p):
         """SampleBatch.shuffle() + one permutation of the minibatch slots per epoch."""
         R = self.T * self.ctx.layout[p]["C"]
         mb = self.cfg.sgd_minibatch_size
-        shuffle = self.rng.permutation(R).astype(np.int32)
+        shuffle = self.sched_rng.permutation(R).astype(np.int32)
         nb = max(1, R // mb)
-        perms = np.stack([self.rng.permutation(nb) for _ in range(self.cfg.num_sgd_iter)]).astype(np.int32)
+        perms = np.stack([self.sched_rng.permutation(nb) for _ in range(self.cfg.num_sgd_iter)]).astype(np.int32)
         return shuffle, perms, nb
 
+    def _learn_ddp(self):
+        torch = self.torch
+        R = self.T * self.ctx.layout[0]["C"]
+        shuffle, perms = self.learner.schedule(self.sched_rng, R, self.cfg.num_sgd_iter)
+        kl = self.learner.learn(torch.from_numpy(shuffle).to(self.device), perms, self.kl_coeff[0], self.grad)
+        nb = perms.shape[1]
+        last = self.ctx.ppo_stats(0, nb).astype(np.float64).mean(0)
+        pid = self.policy_ids[0]
+        learner = {pid: {"cur_kl_coeff": float(np.float32(self.kl_coeff[0])),
+                         "cur_lr": float(np.float32(self.cfg.lr)), "total_loss": last[0],
+                         "policy_loss": last[1], "vf_loss": last[2], "kl": kl, "entropy": last[4],
+                         "vf_explained_var": last[5], "entropy_coeff": self.cfg.entropy_coeff,
+                         "num_ranks": self.world}}
+        self.kl_coeff[0] = update_kl(self.kl_coeff[0], kl, self.config["kl_target"])
+        return learner
+
     def _learn(self):
+        if self.parallel == "ddp":
+            return self._learn_ddp()
         torch = self.torch
         P = self.cfg.n_policies
         sh, pe, nbs = [], [], []

@@ -98,6 +98,11 @@ int ddrl_adam_get(ddrl_ctx* ctx, int pid, float* m_host, float* v_host, size_t n
                   float* beta1_power, float* beta2_power);
 int ddrl_filter_set(ddrl_ctx* ctx, double n, const double* mean_host, const double* sq_host);
 int ddrl_filter_get(ddrl_ctx* ctx, double* n, double* mean_host, double* sq_host);
+/* Pushes since the last ddrl_filter_delta_reset, as their own running stat (RLlib's filter
+ * "buffer"); a data-parallel trainer merges every rank's delta into the synced filter
+ * (RunningStat.update in rank order) and resets (synchronize_filters, P_Local:160). */
+int ddrl_filter_delta_get(ddrl_ctx* ctx, double* n, double* mean_host, double* sq_host);
+int ddrl_filter_delta_reset(ddrl_ctx* ctx);
 
 /* Rollout (per env step).
  * observe: env-side MeanStdFilter push + normalize + per-agent routing of the raw
@@ -120,6 +125,9 @@ int ddrl_step_host(ddrl_ctx* ctx, int t, const float* obs_host, const float* eps
 /* Postprocessing: GAE over the fragment for every policy + advantage standardization
  * statistics (a11/a12). */
 int ddrl_gae(ddrl_ctx* ctx);
+/* fp64 {sum adv, sum adv^2, count} of policy pid from the last ddrl_gae, for a cross-rank
+ * StandardizeFields (the global {mean, max(1e-4, std)} goes back through adv_norm_set). */
+int ddrl_adv_sums_get(ddrl_ctx* ctx, int pid, double* host3);
 
 /* PPO update of policy pid_mask bits (a13-a17).  Per policy p (bit p set):
  *   shuffle_dev[p] : int32[R_p] row permutation (SampleBatch.shuffle)
@@ -136,9 +144,10 @@ int ddrl_ppo_stats(ddrl_ctx* ctx, int pid, float* host, size_t n_steps);
 
 /* Data-parallel (shared policy) primitives: gradient of (1/minibatch) * sum over the
  * given rows -> grad_dev[n_params]; after the caller's all-reduce (RCCL), apply clip +
- * Adam.  rows_dev holds n_rows (<= 128) record indices. */
+ * Adam.  rows_dev holds n_rows (<= 128) record indices.  stats_step >= 0 also writes this
+ * rank's loss statistics of the rows (means over n_rows) into stats row stats_step. */
 int ddrl_ppo_grad(ddrl_ctx* ctx, int pid, const int32_t* rows_dev, int n_rows,
-                  float kl_coeff, float* grad_dev);
+                  float kl_coeff, float* grad_dev, int stats_step);
 int ddrl_ppo_apply(ddrl_ctx* ctx, int pid, const float* grad_dev);
 
 /* Model forward (ModelV2.forward + value_function) on arbitrary rows:

@@ -1,0 +1,195 @@
+"""Data-parallel learner (ddrl_amd.ddp) on CPU: world_size-2 gloo process groups.
+
+The learner is driven with an oracle backend (gradients / clip + Adam from the numpy
+oracle, scaled to 1 / sgd_minibatch_size like ddrl_ppo_grad), so these tests check the
+distributed logic itself -- row shares, gradient all-reduce, identical Adam on every rank,
+filter synchronization, cross-rank StandardizeFields, KL all-reduce -- against a
+single-process oracle run on the union of the ranks' data.
+Tolerances: fp64 statistics 1e-12 relative; parameters as the GPU learner tests
+(>= 99.9 % within 1e-5, max <= 2 lr steps) since the two-half gradient sum differs from
+the one-pass sum by fp32 rounding only.
+"""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+
+from oracle import ddrl_oracle as O
+
+D, A, MB = 19, 2, 128
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_batch(rank, rows):
+    rng = np.random.default_rng(10 + rank)
+    f = np.float32
+    logits = np.concatenate([rng.normal(size=(rows, A)) * 0.3, rng.normal(size=(rows, A)) * 0.1 - 0.5], 1)
+    return dict(obs=rng.normal(size=(rows, D)).astype(f), actions=rng.normal(size=(rows, A)).astype(f),
+                logits=logits.astype(f), logp=(rng.normal(size=rows) - 2).astype(f),
+                vf_preds=rng.normal(size=rows).astype(f), adv=rng.normal(size=rows).astype(f),
+                vt=rng.normal(size=rows).astype(f))
+
+
+class OracleBackend:
+    def __init__(self, params, shapes, batch, cap):
+        self.shapes, self.batch = shapes, batch
+        self.theta = O.pack(params, shapes)
+        self.adam = O.Adam(self.theta.size)
+        self.st = np.zeros((cap, 8), np.float32)
+
+    def grad(self, pid, rows, n_rows, kl, grad, stats_step):
+        import torch
+        rows = np.asarray(rows)
+        b = {k: v[rows] for k, v in self.batch.items()}
+        p = O.unpack(self.theta, self.shapes)
+        logits, value, cache = O.ffn_forward(p, b["obs"])
+        dl, dv, st = O.ppo_loss_rows(logits, value, b["actions"], b["logits"], b["logp"], b["vf_preds"],
+                                     b["adv"], b["vt"], np.float32(kl))
+        s = np.float32(n_rows / MB)          # oracle averages over n_rows; ppo_grad uses 1/128
+        g = O.pack(O.ffn_backward(p, cache, dl * s, dv * s), self.shapes)
+        grad.copy_(torch.from_numpy(g))
+        if stats_step >= 0:
+            self.st[stats_step, 3] = st["kl"]
+
+    def apply(self, pid, grad):
+        clipped, _ = O.clip_by_global_norm([grad.numpy()], 0.5)
+        self.theta = self.adam.apply(self.theta, clipped[0])
+
+    def stats(self, pid, n):
+        return self.st[:n]
+
+
+def _worker(rank, world, port, out_dir, mode, rows_local, epochs):
+    import torch
+    import torch.distributed as dist
+    from ddrl_amd.ddp import Comm, DataParallelLearner, sync_filters, sync_standardize
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = Comm("cpu")
+    # --- filter synchronization: base filter + each rank's pushes since the sync
+    rng = np.random.default_rng(0)
+    base_rs = O.RunningStat((43,))
+    for x in rng.normal(size=(50, 43)):
+        base_rs.push(x)
+    mine = O.RunningStat((43,))
+    for x in np.random.default_rng(100 + rank).normal(size=(30 + 7 * rank, 43)) * 2 + rank:
+        mine.push(x)
+    merged = sync_filters(comm, (base_rs.n, base_rs.M, base_rs.S), (mine.n, mine.M, mine.S))
+    # --- StandardizeFields over the union
+    adv = np.random.default_rng(200 + rank).normal(size=500 + 100 * rank).astype(np.float32) * 3 + 1
+    sums = np.array([np.sum(adv, dtype=np.float64), np.sum(adv.astype(np.float64) ** 2), adv.size])
+    mean, den = sync_standardize(comm, sums)
+    # --- minibatch SGD
+    params = O.ffn_init(np.random.default_rng(7), D, 2 * A)
+    shapes = O.ffn_param_shapes(D, 2 * A)
+    batch = _rank_batch(rank, rows_local)
+    be = OracleBackend(params, shapes, batch, cap=1024)
+    learner = DataParallelLearner(be, comm, minibatch=MB, mode=mode)
+    shuffle, perms = learner.schedule(np.random.default_rng(300 + rank), rows_local, epochs)
+    grad = torch.zeros(be.theta.size)
+    kl = learner.learn(shuffle, perms, 0.2, grad)
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), theta=be.theta, shuffle=shuffle, perms=perms,
+             n=merged[0], M=merged[1], S=merged[2], mean=mean, den=den, kl=kl)
+    dist.destroy_process_group()
+
+
+def _run(mode, rows_local, epochs):
+    import torch.multiprocessing as mp
+    out = tempfile.mkdtemp()
+    mp.spawn(_worker, args=(2, _free_port(), out, mode, rows_local, epochs), nprocs=2, join=True)
+    return [dict(np.load(os.path.join(out, f"r{r}.npz"))) for r in range(2)]
+
+
+def _reference(res, mode, rows_local, epochs):
+    """Single process: the union of both ranks' rows per step, one 128-row (split) or
+    256-row (local) minibatch gradient, clip + Adam."""
+    world = 2
+    m = MB // world if mode == "split" else MB
+    batches = [_rank_batch(r, rows_local) for r in range(world)]
+    full = {k: np.concatenate([b[k] for b in batches]) for k in batches[0]}
+    params = O.ffn_init(np.random.default_rng(7), D, 2 * A)
+    shapes = O.ffn_param_shapes(D, 2 * A)
+    theta = O.pack(params, shapes)
+    adam = O.Adam(theta.size)
+    E, nb = res[0]["perms"].shape
+    kls = []
+    for e in range(E):
+        for b in range(nb):
+            rows = np.concatenate([r * rows_local + res[r]["shuffle"][int(res[r]["perms"][e, b]) * m:
+                                                                      int(res[r]["perms"][e, b]) * m + m]
+                                   for r in range(world)])
+            p = O.unpack(theta, shapes)
+            sl = {k: v[rows] for k, v in full.items()}
+            logits, value, cache = O.ffn_forward(p, sl["obs"])
+            dl, dv, st = O.ppo_loss_rows(logits, value, sl["actions"], sl["logits"], sl["logp"],
+                                         sl["vf_preds"], sl["adv"], sl["vt"], np.float32(0.2))
+            g = O.pack(O.ffn_backward(p, cache, dl, dv), shapes)   # mean over the union rows
+            clipped, _ = O.clip_by_global_norm([g], 0.5)
+            theta = adam.apply(theta, clipped[0])
+            if e == E - 1:
+                kls.append(st["kl"])
+    return theta, float(np.mean(kls))
+
+
+def _params_close(got, ref, steps):
+    diff = np.abs(got - ref)
+    assert np.mean(diff <= 1e-5 + 1e-5 * np.abs(ref)) >= 0.999, diff.max()
+    assert diff.max() <= 2 * 3e-4 * steps + 1e-5
+
+
+@pytest.mark.parametrize("mode", ["split", "local"])
+def test_ddp_learner_world2(mode):
+    rows_local, epochs = 512, 2
+    res = _run(mode, rows_local, epochs)
+    # identical parameters on both ranks (same all-reduced gradient, same Adam)
+    np.testing.assert_array_equal(res[0]["theta"], res[1]["theta"])
+    ref, kl_ref = _reference(res, mode, rows_local, epochs)
+    steps = res[0]["perms"].size
+    _params_close(res[0]["theta"], ref, steps)
+    np.testing.assert_allclose(res[0]["kl"], kl_ref, rtol=1e-5)
+    assert res[0]["kl"] == res[1]["kl"]
+    if mode == "split":
+        # filter sync == one RunningStat over base + rank 0 + rank 1 pushes
+        rs = O.RunningStat((43,))
+        for x in np.random.default_rng(0).normal(size=(50, 43)):
+            rs.push(x)
+        for r in range(2):
+            for x in np.random.default_rng(100 + r).normal(size=(30 + 7 * r, 43)) * 2 + r:
+                rs.push(x)
+        for r in range(2):
+            assert res[r]["n"] == rs.n
+            np.testing.assert_allclose(res[r]["M"], rs.M, rtol=1e-12, atol=1e-12)
+            np.testing.assert_allclose(res[r]["S"], rs.S, rtol=1e-11)
+        adv = np.concatenate([np.random.default_rng(200 + r).normal(size=500 + 100 * r).astype(np.float32) * 3 + 1
+                              for r in range(2)])
+        _, mean, std = O.standardize(adv)
+        assert res[0]["mean"] == res[1]["mean"] and res[0]["den"] == res[1]["den"]
+        np.testing.assert_allclose(res[0]["mean"], mean, rtol=1e-6)
+        np.testing.assert_allclose(res[0]["den"], max(np.float32(1e-4), std), rtol=1e-6)
+
+
+def test_merge_running_stats_order_and_identity():
+    from ddrl_amd.ddp import merge_running_stats
+    rng = np.random.default_rng(1)
+    a, b = O.RunningStat((5,)), O.RunningStat((5,))
+    for x in rng.normal(size=(20, 5)):
+        a.push(x)
+    for x in rng.normal(size=(13, 5)) + 3:
+        b.push(x)
+    n, M, S = merge_running_stats((a.n, a.M, a.S), [(0, np.zeros(5), np.zeros(5)), (b.n, b.M, b.S)])
+    ref = O.RunningStat((5,))
+    ref.n, ref.M[:], ref.S[:] = a.n, a.M, a.S
+    ref.update(b)
+    assert n == ref.n
+    np.testing.assert_allclose(M, ref.M, rtol=1e-14)
+    np.testing.assert_allclose(S, ref.S, rtol=1e-14)
