@@ -37,6 +37,34 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// Global-memory access through address space 1.  Pointers read from argument arrays are
+// generic to the compiler, which then emits flat_* instructions; flat loads count against
+// lgkmcnt as well as vmcnt, so every later LDS wait would also wait for them.
+template <class T>
+__device__ __forceinline__ T gld(const T* p) {
+  return *(const __attribute__((address_space(1))) T*)p;
+}
+template <class T>
+__device__ __forceinline__ void gst(T* p, T v) {
+  *(__attribute__((address_space(1))) T*)p = v;
+}
+
+// LDS byte address of a pointer into __shared__ memory.
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(size_t)(const __attribute__((address_space(3))) void*)p;
+}
+// LDS-DMA: 16 bytes per lane from gsrc into LDS at the wave-uniform byte address lds_dst +
+// 16 * lane (global_load_lds_dwordx4).  Invisible to the compiler's s_waitcnt bookkeeping:
+// the caller waits vmcnt itself before a barrier and the ds_reads of the data.
+__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+__device__ __forceinline__ void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 __device__ __forceinline__ floatx4 splat4(float v) { floatx4 r = {v, v, v, v}; return r; }
 
 // tanh as 1 - 2 / (2^(2 log2(e) |x|) + 1) with the hardware exp2 / reciprocal, sign copied

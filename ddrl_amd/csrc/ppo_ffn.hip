@@ -81,31 +81,57 @@ struct RowData {
   float s0[2], s1[2];  // policy: logp_old, adv;  value: vf_old, vt
 };
 
+// The next minibatch's 128 records are gathered by LDS-DMA into stg [128][stride] while the
+// current step computes: 16-byte chunk g of the gather is record column 4 (g % cpr) of row
+// g / cpr (cpr = stride / 4), and one wave-instruction writes 64 consecutive chunks (the
+// lane-linear LDS destination of global_load_lds).  Whole 64-byte record lines instead of
+// per-lane dword gathers: 3 line requests per row rather than one per field and lane.
+// The staging rows hold cpr_l = cpr | 1 chunks (an odd number: the 16 rows a lane group
+// reads then start in 16 different banks); the pad chunk repeats the row's last chunk.
+__device__ __forceinline__ void issue_rows(const float* rec, int stride, int cpr, int cpr_l, const int* idxb,
+                                           float* stg) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nchunk = DDRL_MB * cpr_l;
+  const float inv = 1.f / (float)cpr_l;
+  for (int base = 64 * w; base < nchunk; base += NT) {   // wave-uniform
+    const int g = base + lane;
+    const int row = (int)(((float)g + 0.5f) * inv);
+    const int k = min(g - row * cpr_l, cpr - 1);
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr(stg + 4 * base));
+    if (g < nchunk) glds16(rec + (size_t)idxb[row] * stride + 4 * k, dst);
+  }
+}
+
+// staging-row chunks for a record of `stride` floats (the A = 8 kernels keep the plain
+// stride: their LDS budget has no room for the pad)
+__host__ __device__ constexpr int stg_chunks(int stride, int A) { return A == 8 ? stride / 4 : (stride / 4) | 1; }
+
+// This lane's two rows from the staged records (padding rows hold record 0; their output
+// gradient is zeroed).  Observation columns f >= d read the record's next (finite) fields,
+// which meet the zero rows of the W1 image; their dW1 rows are never stored.
 template <int A, int KS1, bool POL>
-__device__ __forceinline__ void load_row(const UpdateArgs& U, const int* ridx, const bool* ok, RowData<A>& r) {
+__device__ __forceinline__ void load_row(const float* stg, int stg_stride, const RecLayout& L, const int* row_l,
+                                         RowData<A>& r) {
   const int q = (threadIdx.x & 63) >> 4;
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
-    const float* rp = U.rec + (size_t)ridx[t] * U.lay.stride;
+    const float* rp = stg + row_l[t] * stg_stride;
 #pragma unroll
-    for (int s = 0; s < 12; ++s) {
-      const int f = 4 * s + q;
-      r.x[t][s] = (ok[t] && s < KS1 && f < U.d) ? rp[U.lay.obs + f] : 0.f;
-    }
+    for (int s = 0; s < 12; ++s) r.x[t][s] = s < KS1 ? rp[L.obs + 4 * s + q] : 0.f;
     if (POL) {
 #pragma unroll
-      for (int j = 0; j < A; ++j) r.act[t][j] = rp[U.lay.act + j];
+      for (int j = 0; j < A; ++j) r.act[t][j] = rp[L.act + j];
 #pragma unroll
-      for (int j = 0; j < 2 * A; ++j) r.ol[t][j] = rp[U.lay.logit + j];
-      r.s0[t] = rp[U.lay.logp];
-      r.s1[t] = rp[U.lay.adv];
+      for (int j = 0; j < 2 * A; ++j) r.ol[t][j] = rp[L.logit + j];
+      r.s0[t] = rp[L.logp];
+      r.s1[t] = rp[L.adv];
     } else {
 #pragma unroll
       for (int j = 0; j < A; ++j) r.act[t][j] = 0.f;
 #pragma unroll
       for (int j = 0; j < 2 * A; ++j) r.ol[t][j] = 0.f;
-      r.s0[t] = rp[U.lay.vf];
-      r.s1[t] = rp[U.lay.vt];
+      r.s0[t] = rp[L.vf];
+      r.s1[t] = rp[L.vt];
     }
   }
 }
@@ -121,33 +147,33 @@ __device__ __forceinline__ void write_stats(float* so, const float* red, float n
     for (int i = 0; i < NW; ++i) sv[k] += red[i * 8 + k];
   }
   if constexpr (POL) {
-    so[1] = sv[0] / n; so[3] = sv[1] / n; so[4] = sv[2] / n;
+    gst(so + 1, sv[0] / n); gst(so + 3, sv[1] / n); gst(so + 4, sv[2] / n);
   } else {
-    so[2] = sv[0] / n;
+    gst(so + 2, sv[0] / n);
     const float vy = sv[2] / n - (sv[1] / n) * (sv[1] / n);
     const float vd = sv[4] / n - (sv[3] / n) * (sv[3] / n);
-    so[5] = vy > 0.f ? fmaxf(-1.f, 1.f - vd / vy) : 0.f;
+    gst(so + 5, vy > 0.f ? fmaxf(-1.f, 1.f - vd / vy) : 0.f);
   }
 }
 
 __device__ __forceinline__ int row_index(const UpdateArgs& U, int step, int row_l, bool ok) {
   if (!ok) return 0;
   const int e = step / U.nb, b = step - e * U.nb;
-  return U.shuffle[U.perm[e * U.nb + b] * DDRL_MB + row_l];
+  return gld(U.shuffle + gld(U.perm + e * U.nb + b) * DDRL_MB + row_l);
 }
 // minibatch slot of a step (wave-uniform: perm[e][b])
 __device__ __forceinline__ int perm_slot(const UpdateArgs& U, int step) {
   const int e = step / U.nb, b = step - e * U.nb;
-  return U.perm[e * U.nb + b];
+  return gld(U.perm + e * U.nb + b);
 }
 
 // Diagnostic build only (-DDDRL_STAMPS): per-phase s_memtime cycle counts of wave 0 of each
 // workgroup, accumulated over the steps of one launch; no stamp executes in the real build.
 #ifdef DDRL_STAMPS
 __device__ unsigned long long g_stamps[2 * DDRL_MAXP][16];
-#define STAMP_INIT unsigned long long st_prev = __builtin_amdgcn_s_memtime(), st_acc[12] = {0};
+#define STAMP_INIT unsigned long long st_prev = __builtin_amdgcn_s_memtime(), st_acc[16] = {0};
 #define STAMP(k) do { if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[k] += t_ - st_prev; st_prev = t_; } } while (0)
-#define STAMP_DONE do { if (tid == 0) for (int k_ = 0; k_ < 12; ++k_) g_stamps[blockIdx.x][k_] = st_acc[k_]; } while (0)
+#define STAMP_DONE do { if (tid == 0) for (int k_ = 0; k_ < 16; ++k_) g_stamps[blockIdx.x][k_] = st_acc[k_]; } while (0)
 extern "C" int ddrl_diag_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) == hipSuccess ? 0 : -1;
 }
@@ -178,6 +204,9 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   float* bufB = bufA + 64 * FM_LD;          // feature-major [64][FM_LD]: dZ2, then dZ1
   float* Pb = bufB + 64 * FM_LD;            // [NW][NSB] per-wave partial small grads
   float* red = Pb + NW * NSB;               // [NW][8] row-stat partials, [64..] scalars
+  int* idxb = reinterpret_cast<int*>(red + 128);   // [128] record rows of the next step
+  float* stg = red + 256;                   // [128][stride] records of the next step (16 B aligned)
+  const int stride = U.lay.stride, cpr = stride >> 2, cpr_l = stg_chunks(stride, A);
 
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, q = lane >> 4, w = tid >> 6;
   int row_l[2];
@@ -232,20 +261,20 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   const int total_steps = U.n_epochs * U.nb;
   const int last = U.max_steps >= 0 ? min(total_steps, U.step0 + U.max_steps) : total_steps;
   RowData<A> cur;
-  int idx_nxt[2] = {0, 0};
-  int slot_nn = 0;   // perm slot of step+2, loaded one step before its shuffle lookup
-  if (U.step0 < last) {
-    int ix[2] = {row_index(U, U.step0, row_l[0], row_ok[0]), row_index(U, U.step0, row_l[1], row_ok[1])};
-    load_row<A, KS1, POL>(U, ix, row_ok, cur);
-  }
-  if (U.step0 + 1 < last) {
-    idx_nxt[0] = row_index(U, U.step0 + 1, row_l[0], row_ok[0]);
-    idx_nxt[1] = row_index(U, U.step0 + 1, row_l[1], row_ok[1]);
-  }
-  if (U.step0 + 2 < last) slot_nn = perm_slot(U, U.step0 + 2);
+  // records of step0 -> stg, row indices of step0 + 1 -> idxb, of step0 + 2 -> nxt
+  const int tr = tid < ub.nrows ? tid : 0;
+  if (tid < DDRL_MB) idxb[tid] = U.step0 < last && tid < ub.nrows ? row_index(U, U.step0, tr, true) : 0;
+  __syncthreads();
+  if (U.step0 < last) issue_rows(U.rec, stride, cpr, cpr_l, idxb, stg);
+  wait_vmcnt0();
+  __syncthreads();
+  if (tid < DDRL_MB) idxb[tid] = U.step0 + 1 < last && tid < ub.nrows ? row_index(U, U.step0 + 1, tr, true) : 0;
+  int nxt = tid < DDRL_MB && U.step0 + 2 < last && tid < ub.nrows ? row_index(U, U.step0 + 2, tr, true) : 0;
+  __syncthreads();
 
   STAMP_INIT
   for (int step = U.step0; step < last; ++step) {
+    load_row<A, KS1, POL>(stg, 4 * cpr_l, U.lay, row_l, cur);
     // ---- forward + loss + output gradient (two row tiles) ----
     floatx4 h1[2][4], h2[2][4], dz[2][4];
     float out[2][OB], dout[2][OB];
@@ -332,6 +361,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     }
     STAMP(6);
     __syncthreads();                                     // #2: dW2 operands consumed
+    STAMP(7);
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       store_act_fm(bufB, 2 * w + t, h2[t]);
@@ -339,14 +369,11 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       for (int s = 0; s < 12; ++s) bufA[(4 * s + q) * FM_LD + row_l[t]] = cur.x[t][s];
     }
     __syncthreads();                                     // #3: X, dZ1 visible
-    // ---- prefetch (the current rows are dead from here on): rows of step+1 land in `cur`
-    //      while the dW1 tiles, the norm exchange and Adam run; indices of step+2 likewise
-    if (step + 1 < last) load_row<A, KS1, POL>(U, idx_nxt, row_ok, cur);
-    if (step + 2 < last) {   // slot_nn arrived during the previous step: no dependent wait
-      idx_nxt[0] = row_ok[0] ? U.shuffle[slot_nn * DDRL_MB + row_l[0]] : 0;
-      idx_nxt[1] = row_ok[1] ? U.shuffle[slot_nn * DDRL_MB + row_l[1]] : 0;
-    }
-    if (step + 3 < last) slot_nn = perm_slot(U, step + 3);
+    STAMP(8);
+    // ---- prefetch: the records of step + 1 land in stg (LDS-DMA) while the dW1 tiles, the
+    //      norm exchange and Adam run; every lane has read its rows of this step (sync #1)
+    if (step + 1 < last) issue_rows(U.rec, stride, cpr, cpr_l, idxb, stg);
+    STAMP(9);
     {
       const int fa3[3] = {0, 1, 2};                     // dW1 tiles (fa < nf1, fo = w)
       gt[4] = gt[5] = gt[6] = splat4(0.f);
@@ -354,7 +381,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       else if (nf1 == 2) dw_tiles_fm<DDRL_MB, 2>(bufA, bufB, fa3, w, gt + 4);
       else dw_tiles_fm<DDRL_MB, 1>(bufA, bufB, fa3, w, gt + 4);
     }
-    STAMP(7);
+    STAMP(10);
     float gs[NSLOT];
     float ss = 0.f;
 #pragma unroll
@@ -425,11 +452,11 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       red[81] = H.grad_clip * fminf(1.f / gn, 1.f / H.grad_clip);
     }
     __syncthreads();                                     // #5
-    STAMP(8);
+    STAMP(11);
     if (U.stats && tid == 64) {   // off the critical path: wave 1, after the exchange
       write_stats<POL, NSTAT>(U.stats + (size_t)step * 8, red, (float)ub.nrows);
-      U.stats[(size_t)step * 8 + 6] = red[80];
-      U.stats[(size_t)step * 8 + 7] = red[81];
+      gst(U.stats + (size_t)step * 8 + 6, red[80]);
+      gst(U.stats + (size_t)step * 8 + 7, red[81]);
     }
     const float scale = red[81];
     const float alpha = H.lr * sqrtf(1.f - b2p) / (1.f - b1p);
@@ -484,9 +511,12 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     }
     b1p = b1p * H.b1;
     b2p = b2p * H.b2;
-    STAMP(9);
-    __syncthreads();                                     // #6: weights updated, buffers free
-    STAMP(10);
+    STAMP(12);
+    wait_vmcnt0();                                       // this wave's record gathers landed
+    if (tid < DDRL_MB) idxb[tid] = nxt;                  // row indices of step + 2
+    __syncthreads();                                     // #6: weights updated, stg / idxb ready
+    if (tid < DDRL_MB) nxt = step + 3 < last && tid < ub.nrows ? row_index(U, step + 3, tr, true) : 0;
+    STAMP(13);
   }
   STAMP_DONE;
   if (U.grad_out) return;
@@ -532,14 +562,15 @@ __global__ void __launch_bounds__(NT) k_update_ffn(UpdateBatch ub) {
   else update_loop<A, KS1, 2 * A, true>(U, ub, lds, p);
 }
 
-static size_t update_lds_bytes(int O) {
+// stride: the widest record stride of the launched policies (staging buffer rows)
+static size_t update_lds_bytes(int O, int stride) {
   const int nsb = 64 * O + O + 128;
-  return (size_t)(BRANCH_LDS_FLOATS + 2 * 64 * FM_LD + NW * nsb + 128) * 4;
+  return (size_t)(BRANCH_LDS_FLOATS + 2 * 64 * FM_LD + NW * nsb + 256 + DDRL_MB * 4 * stg_chunks(stride, O / 2)) * 4;
 }
 
 template <int A, int KS1>
-static void launch_update_t(hipStream_t s, const UpdateBatch& ub, int P) {
-  hipLaunchKernelGGL((k_update_ffn<A, KS1>), dim3(2 * P), dim3(NT), update_lds_bytes(2 * A), s, ub);
+static void launch_update_t(hipStream_t s, const UpdateBatch& ub, int P, int stride) {
+  hipLaunchKernelGGL((k_update_ffn<A, KS1>), dim3(2 * P), dim3(NT), update_lds_bytes(2 * A, stride), s, ub);
 }
 
 void launch_update_ffn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHyper& h, int nrows, float inv_n,
@@ -552,7 +583,8 @@ void launch_update_ffn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHype
   ub.xchg = xchg;
   ub.err = err;
   (void)hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * 4 * h.P, s);
-  DDRL_DISPATCH_A_KS1(A, d, launch_update_t, s, ub, h.P);
+  const int stride = (d + 3 * A + 5 + 3) & ~3;   // RecLayout stride of the widest policy (capi make_layout)
+  DDRL_DISPATCH_A_KS1(A, d, launch_update_t, s, ub, h.P, stride);
 }
 
 // ------------------------------------------------------------------------------------

@@ -4,7 +4,11 @@ import ctypes, os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 from ddrl_amd import build, native as N
-lib = build.build(extra_flags=["-DDDRL_STAMPS"], lib=os.path.join(os.path.dirname(N.LIB_PATH), "libddrl_hip_diag.so"))
+extra = os.environ.get("DDRL_EXTRA_FLAGS", "").split()
+tag = "".join(ch for ch in "".join(extra) if ch.isalnum())[:24]
+lib = build.build(extra_flags=["-DDDRL_STAMPS"] + extra,
+                  lib=os.path.join(os.path.dirname(N.LIB_PATH), f"libddrl_hip_diag{tag}.so"),
+                  build_dir=os.path.join(os.path.dirname(N.LIB_PATH), f"_build_diag{tag}"))
 N.load(lib)
 from ddrl_amd.spec import make_cfg
 from ddrl_amd.trainer import glorot_ffn_flat
@@ -31,9 +35,10 @@ for it in range(2):
     dt = time.perf_counter() - t0
 st = (ctypes.c_ulonglong * (8 * 16))()
 assert N.load().ddrl_diag_stamps(st) == 0
-a = np.array(st, dtype=np.float64).reshape(8, 16)[:, :11] / steps
+a = np.array(st, dtype=np.float64).reshape(8, 16)[:, :14] / steps
 names = ["fwd", "loss", "dpp head/bias", "head bwd+db2+stores", "layer2 bwd+db1", "sync#1",
-         "dW2 tiles", "sync#2,#3+X/dZ1 stores+dW1 tiles+prefetch", "norm+exchange", "adam", "sync#6"]
+         "dW2 tiles", "sync#2", "X/dZ1 stores + sync#3", "prefetch issue", "dW1 tiles",
+         "norm+exchange", "adam", "sync#6"]
 print(f"steps {steps}, {dt / steps * 1e6:.2f} us/step wall")
 for wg in (0, 1):
     tot = a[wg].sum()
