@@ -23,8 +23,16 @@
 #include "ffn.h"
 #include "ppo_loss.h"
 
-#define NT 256   // 4 waves: one per SIMD, 32 rows (two 16-row tiles) each
-#define NW 4
+// Workgroup geometry: NW waves (8 = two per SIMD with one 16-row tile each; the A = 8
+// kernels use 4 waves with two tiles each, their per-wave head partials would not fit LDS).
+template <int NW>
+struct Geo {
+  static constexpr int NT = 64 * NW;
+  static constexpr int RT = DDRL_MB / (16 * NW);   // 16-row tiles per wave
+  static constexpr int NS1 = 16 / NW;              // dW2 tile slots per wave (16 tiles)
+  static constexpr int NS2 = (12 + NW - 1) / NW;   // dW1 tile slots per wave (<= 12 tiles)
+};
+__host__ __device__ constexpr int waves_for(int A) { return A == 8 ? 4 : 8; }
 
 struct UpdateBatch {
   const UpdateArgs* a;   // device array, one entry per policy
@@ -50,14 +58,14 @@ __device__ void stage_branch(const float* __restrict__ th, int d, const BranchOf
                              NetLds& W) {
   W.w1 = lds; W.w2 = W.w1 + 48 * 64; W.b1 = W.w2 + 64 * 64; W.b2 = W.b1 + 64;
   W.wo = W.b2 + 64; W.bo = W.wo + 64 * OB;
-  for (int i = threadIdx.x; i < 48 * 64; i += NT) {
+  for (int i = threadIdx.x; i < 48 * 64; i += blockDim.x) {
     const int f = i >> 6;
     W.w1[sidx(f, i & 63)] = f < d ? th[bo.w1 + i] : 0.f;
   }
-  for (int i = threadIdx.x; i < 64 * 64; i += NT) W.w2[sidx(i >> 6, i & 63)] = th[bo.w2 + i];
-  for (int i = threadIdx.x; i < 64; i += NT) { W.b1[i] = th[bo.b1 + i]; W.b2[i] = th[bo.b2 + i]; }
-  for (int i = threadIdx.x; i < 64 * OB; i += NT) W.wo[i] = th[bo.wo + i];
-  for (int i = threadIdx.x; i < OB; i += NT) W.bo[i] = th[bo.bo + i];
+  for (int i = threadIdx.x; i < 64 * 64; i += blockDim.x) W.w2[sidx(i >> 6, i & 63)] = th[bo.w2 + i];
+  for (int i = threadIdx.x; i < 64; i += blockDim.x) { W.b1[i] = th[bo.b1 + i]; W.b2[i] = th[bo.b2 + i]; }
+  for (int i = threadIdx.x; i < 64 * OB; i += blockDim.x) W.wo[i] = th[bo.wo + i];
+  for (int i = threadIdx.x; i < OB; i += blockDim.x) W.bo[i] = th[bo.bo + i];
 }
 #define BRANCH_LDS_FLOATS (48 * 64 + 64 * 64 + 128 + 64 * 16 + 16)   // multiple of 4 floats
 
@@ -73,12 +81,12 @@ __device__ __forceinline__ void small_param(int e, const BranchOff& bo, const Ne
   pidx = bo.b2 + e; lp = W.b2 + e;
 }
 
-template <int A>
+template <int A, int RT>
 struct RowData {
-  float x[2][12];      // two row tiles
-  float act[2][A];
-  float ol[2][2 * A];
-  float s0[2], s1[2];  // policy: logp_old, adv;  value: vf_old, vt
+  float x[RT][12];      // this wave's row tiles
+  float act[RT][A];
+  float ol[RT][2 * A];
+  float s0[RT], s1[RT];  // policy: logp_old, adv;  value: vf_old, vt
 };
 
 // The next minibatch's 128 records are gathered by LDS-DMA into stg [128][stride] while the
@@ -88,6 +96,7 @@ struct RowData {
 // per-lane dword gathers: 3 line requests per row rather than one per field and lane.
 // The staging rows hold cpr_l = cpr | 1 chunks (an odd number: the 16 rows a lane group
 // reads then start in 16 different banks); the pad chunk repeats the row's last chunk.
+template <int NT>
 __device__ __forceinline__ void issue_rows(const float* rec, int stride, int cpr, int cpr_l, const int* idxb,
                                            float* stg) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -109,12 +118,12 @@ __host__ __device__ constexpr int stg_chunks(int stride, int A) { return A == 8 
 // This lane's two rows from the staged records (padding rows hold record 0; their output
 // gradient is zeroed).  Observation columns f >= d read the record's next (finite) fields,
 // which meet the zero rows of the W1 image; their dW1 rows are never stored.
-template <int A, int KS1, bool POL>
+template <int A, int KS1, bool POL, int RT>
 __device__ __forceinline__ void load_row(const float* stg, int stg_stride, const RecLayout& L, const int* row_l,
-                                         RowData<A>& r) {
+                                         RowData<A, RT>& r) {
   const int q = (threadIdx.x & 63) >> 4;
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
+  for (int t = 0; t < RT; ++t) {
     const float* rp = stg + row_l[t] * stg_stride;
 #pragma unroll
     for (int s = 0; s < 12; ++s) r.x[t][s] = s < KS1 ? rp[L.obs + 4 * s + q] : 0.f;
@@ -138,7 +147,7 @@ __device__ __forceinline__ void load_row(const float* stg, int stg_stride, const
 
 // Per-step learner statistics from the per-wave partial sums red[w * 8 + k]: policy
 // workgroup -> policy_loss, kl, entropy; value workgroup -> vf_loss, vf_explained_var.
-template <bool POL, int NSTAT>
+template <bool POL, int NSTAT, int NW>
 __device__ __forceinline__ void write_stats(float* so, const float* red, float n) {
   float sv[NSTAT];
 #pragma unroll
@@ -183,11 +192,9 @@ extern "C" int ddrl_diag_stamps(unsigned long long* host) {
 #define STAMP_DONE
 #endif
 
-#define NS1 4   // dW2 tile slots per wave (16 tiles / 4 waves)
-#define NS2 3   // dW1 tile slots per wave (<= 12 tiles / 4 waves)
-
-template <int A, int KS1, int OB, bool POL>
+template <int A, int KS1, int OB, bool POL, int NW>
 __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBatch& ub, float* lds, int p) {
+  constexpr int NT = Geo<NW>::NT, RT = Geo<NW>::RT, NS1 = Geo<NW>::NS1, NS2 = Geo<NW>::NS2;
   const UpdateHyper& H = ub.h;
   const int d = U.d;
   const FfnOffsets of = ffn_offsets(d, A);
@@ -209,22 +216,23 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   const int stride = U.lay.stride, cpr = stride >> 2, cpr_l = stg_chunks(stride, A);
 
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, q = lane >> 4, w = tid >> 6;
-  int row_l[2];
-  bool row_ok[2];
+  int row_l[RT];
+  bool row_ok[RT];
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    row_l[t] = 32 * w + 16 * t + c;
+  for (int t = 0; t < RT; ++t) {
+    row_l[t] = 16 * RT * w + 16 * t + c;
     row_ok[t] = row_l[t] < ub.nrows;
   }
 
   // ---- optimizer state of the parameters this lane owns ----
-  // slots 0..3: dW2 tiles w, w+4, w+8, w+12;  slots 4..6: dW1 tiles w, w+4, w+8 (if < 4*nf1)
+  // tile tt = 4 fa + fo; slots 0..NS1-1: dW2 tiles w + NW i;  then dW1 tiles w + NW i (if < 4 nf1).
+  // NW is a multiple of 4, so every tile of a wave has fo = w & 3.
   floatx4 mt[NTS], vt4[NTS];
   bool tv[NTS];
   int tfa[NTS], tfo[NTS];
 #pragma unroll
   for (int i = 0; i < NTS; ++i) {
-    const int tt = i < NS1 ? w + 4 * i : w + 4 * (i - NS1);
+    const int tt = i < NS1 ? w + NW * i : w + NW * (i - NS1);
     tv[i] = i < NS1 ? true : (tt < 4 * nf1);
     tfa[i] = tt >> 2;
     tfo[i] = tt & 3;
@@ -251,7 +259,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   }
   int ebase[4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) ebase[r] = sidx(4 * q + r, 16 * w + c);
+  for (int r = 0; r < 4; ++r) ebase[r] = sidx(4 * q + r, 16 * (w & 3) + c);
   float b1p = U.beta_pow[0], b2p = U.beta_pow[1];
   const float adv_mean = U.adv_norm[0], adv_den = U.adv_norm[1];
   const float beta = U.kl_coeff;
@@ -260,12 +268,12 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 
   const int total_steps = U.n_epochs * U.nb;
   const int last = U.max_steps >= 0 ? min(total_steps, U.step0 + U.max_steps) : total_steps;
-  RowData<A> cur;
+  RowData<A, RT> cur;
   // records of step0 -> stg, row indices of step0 + 1 -> idxb, of step0 + 2 -> nxt
   const int tr = tid < ub.nrows ? tid : 0;
   if (tid < DDRL_MB) idxb[tid] = U.step0 < last && tid < ub.nrows ? row_index(U, U.step0, tr, true) : 0;
   __syncthreads();
-  if (U.step0 < last) issue_rows(U.rec, stride, cpr, cpr_l, idxb, stg);
+  if (U.step0 < last) issue_rows<NT>(U.rec, stride, cpr, cpr_l, idxb, stg);
   wait_vmcnt0();
   __syncthreads();
   if (tid < DDRL_MB) idxb[tid] = U.step0 + 1 < last && tid < ub.nrows ? row_index(U, U.step0 + 1, tr, true) : 0;
@@ -274,30 +282,29 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 
   STAMP_INIT
   for (int step = U.step0; step < last; ++step) {
-    load_row<A, KS1, POL>(stg, 4 * cpr_l, U.lay, row_l, cur);
+    load_row<A, KS1, POL, RT>(stg, 4 * cpr_l, U.lay, row_l, cur);
     // ---- forward + loss + output gradient (two row tiles) ----
-    floatx4 h1[2][4], h2[2][4], dz[2][4];
-    float out[2][OB], dout[2][OB];
-    ffn_fwd_rt<OB, KS1, 2>(W, cur.x, h1, h2, out);
+    floatx4 h1[RT][4], h2[RT][4], dz[RT][4];
+    float out[RT][OB], dout[RT][OB];
+    ffn_fwd_rt<OB, KS1, RT>(W, cur.x, h1, h2, out);
     STAMP(0);
     float st[NSTAT];
-    {
-      float st0[NSTAT], st1[NSTAT];
-      if constexpr (POL) {
-        policy_loss_row<A>(out[0], cur.act[0], cur.ol[0], cur.s0[0], (cur.s1[0] - adv_mean) / adv_den,
-                           beta, lo, hi, H.ent_coeff, ub.inv_n, row_ok[0], dout[0], st0);
-        policy_loss_row<A>(out[1], cur.act[1], cur.ol[1], cur.s0[1], (cur.s1[1] - adv_mean) / adv_den,
-                           beta, lo, hi, H.ent_coeff, ub.inv_n, row_ok[1], dout[1], st1);
-      } else {
-        value_loss_row(out[0][0], cur.s0[0], cur.s1[0], H, ub.inv_n, row_ok[0], dout[0], st0);
-        value_loss_row(out[1][0], cur.s0[1], cur.s1[1], H, ub.inv_n, row_ok[1], dout[1], st1);
-      }
 #pragma unroll
-      for (int k = 0; k < NSTAT; ++k) st[k] = st0[k] + st1[k];
+    for (int k = 0; k < NSTAT; ++k) st[k] = 0.f;
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      float st0[NSTAT];
+      if constexpr (POL)
+        policy_loss_row<A>(out[t], cur.act[t], cur.ol[t], cur.s0[t], (cur.s1[t] - adv_mean) / adv_den,
+                           beta, lo, hi, H.ent_coeff, ub.inv_n, row_ok[t], dout[t], st0);
+      else
+        value_loss_row(out[t][0], cur.s0[t], cur.s1[t], H, ub.inv_n, row_ok[t], dout[t], st0);
+#pragma unroll
+      for (int k = 0; k < NSTAT; ++k) st[k] += st0[k];
     }
     STAMP(1);
     float* Pw = Pb + w * NSB;
-    // head weight / bias partial gradients over this wave's 32 rows: DPP transpose-reduce
+    // head weight / bias partial gradients over this wave's rows: DPP transpose-reduce
     // of the 16 features (fb, r) a lane holds; afterwards lane (c, q) owns feature
     // h = 16 (c >> 2) + 4 q + (c & 3).
     const int h_own = 16 * (c >> 2) + 4 * q + (c & 3);
@@ -307,12 +314,19 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 #pragma unroll
       for (int fb = 0; fb < 4; ++fb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[4 * fb + r] = h2[0][fb][r] * dout[0][o] + h2[1][fb][r] * dout[1][o];
+        for (int r = 0; r < 4; ++r) {
+          v[4 * fb + r] = h2[0][fb][r] * dout[0][o];
+#pragma unroll
+          for (int t = 1; t < RT; ++t) v[4 * fb + r] += h2[t][fb][r] * dout[t][o];
+        }
       Pw[h_own * OB + o] = row16_transpose_sum(v);
     }
 #pragma unroll
     for (int o = 0; o < OB; ++o) {
-      const float s = row16_sum(dout[0][o] + dout[1][o]);
+      float dsum = dout[0][o];
+#pragma unroll
+      for (int t = 1; t < RT; ++t) dsum += dout[t][o];
+      const float s = row16_sum(dsum);
       if (lane == 0) Pw[64 * OB + o] = s;
     }
 #pragma unroll
@@ -322,7 +336,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     }
     STAMP(2);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < RT; ++t) {
       head_bwd<OB>(W, dout[t], dz[t]);
       dtanh_inplace(dz[t], h2[t]);                       // dz = dZ2
     }
@@ -331,40 +345,45 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 #pragma unroll
       for (int fb = 0; fb < 4; ++fb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[4 * fb + r] = dz[0][fb][r] + dz[1][fb][r];
+        for (int r = 0; r < 4; ++r) {
+          v[4 * fb + r] = dz[0][fb][r];
+#pragma unroll
+          for (int t = 1; t < RT; ++t) v[4 * fb + r] += dz[t][fb][r];
+        }
       Pw[64 * OB + OB + 64 + h_own] = row16_transpose_sum(v);     // db2
     }
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      store_act_fm(bufA, 2 * w + t, h1[t]);
-      store_act_fm(bufB, 2 * w + t, dz[t]);
+    for (int t = 0; t < RT; ++t) {
+      store_act_fm(bufA, RT * w + t, h1[t]);
+      store_act_fm(bufB, RT * w + t, dz[t]);
     }
     STAMP(3);
-    layer2_bwd_rt<2>(W, dz, h2);                         // h2 <- dH1
+    layer2_bwd_rt<RT>(W, dz, h2);                        // h2 <- dH1
 #pragma unroll
-    for (int t = 0; t < 2; ++t) dtanh_inplace(h2[t], h1[t]);   // h2 = dZ1
+    for (int t = 0; t < RT; ++t) dtanh_inplace(h2[t], h1[t]);  // h2 = dZ1
     {
       float v[16];
 #pragma unroll
       for (int fb = 0; fb < 4; ++fb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[4 * fb + r] = h2[0][fb][r] + h2[1][fb][r];
+        for (int r = 0; r < 4; ++r) {
+          v[4 * fb + r] = h2[0][fb][r];
+#pragma unroll
+          for (int t = 1; t < RT; ++t) v[4 * fb + r] += h2[t][fb][r];
+        }
       Pw[64 * OB + OB + h_own] = row16_transpose_sum(v);          // db1
     }
     STAMP(4);
     __syncthreads();                                     // #1: H1, dZ2, partials visible
     STAMP(5);
     floatx4 gt[NTS];
-    {
-      const int fa4[4] = {0, 1, 2, 3};
-      dw_tiles_fm<DDRL_MB, 4>(bufA, bufB, fa4, w, gt);   // dW2 tiles (fa = 0..3, fo = w)
-    }
+    dw_tiles_fm<DDRL_MB, NS1>(bufA, bufB, tfa, w & 3, gt);   // dW2 tiles of this wave
     STAMP(6);
     __syncthreads();                                     // #2: dW2 operands consumed
     STAMP(7);
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      store_act_fm(bufB, 2 * w + t, h2[t]);
+    for (int t = 0; t < RT; ++t) {
+      store_act_fm(bufB, RT * w + t, h2[t]);
 #pragma unroll
       for (int s = 0; s < 12; ++s) bufA[(4 * s + q) * FM_LD + row_l[t]] = cur.x[t][s];
     }
@@ -372,14 +391,20 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     STAMP(8);
     // ---- prefetch: the records of step + 1 land in stg (LDS-DMA) while the dW1 tiles, the
     //      norm exchange and Adam run; every lane has read its rows of this step (sync #1)
-    if (step + 1 < last) issue_rows(U.rec, stride, cpr, cpr_l, idxb, stg);
+    if (step + 1 < last) issue_rows<NT>(U.rec, stride, cpr, cpr_l, idxb, stg);
     STAMP(9);
     {
-      const int fa3[3] = {0, 1, 2};                     // dW1 tiles (fa < nf1, fo = w)
-      gt[4] = gt[5] = gt[6] = splat4(0.f);
-      if (nf1 >= 3) dw_tiles_fm<DDRL_MB, 3>(bufA, bufB, fa3, w, gt + 4);
-      else if (nf1 == 2) dw_tiles_fm<DDRL_MB, 2>(bufA, bufB, fa3, w, gt + 4);
-      else dw_tiles_fm<DDRL_MB, 1>(bufA, bufB, fa3, w, gt + 4);
+      // dW1 tiles of this wave: the valid slots are a prefix (tiles w + NW i < 4 nf1)
+#pragma unroll
+      for (int i = NS1; i < NTS; ++i) gt[i] = splat4(0.f);
+      int n1 = 0;
+#pragma unroll
+      for (int i = NS1; i < NTS; ++i) n1 += tv[i] ? 1 : 0;
+      if (n1 == NS2) dw_tiles_fm<DDRL_MB, NS2>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
+      else if constexpr (NS2 >= 3) {
+        if (n1 == 2) dw_tiles_fm<DDRL_MB, 2>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
+        else if (n1 == 1) dw_tiles_fm<DDRL_MB, 1>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
+      } else if (n1 == 1) dw_tiles_fm<DDRL_MB, 1>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
     }
     STAMP(10);
     float gs[NSLOT];
@@ -418,7 +443,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
           U.grad_out[pidx] = gs[k];
         }
       }
-      if (U.stats && tid == 64) write_stats<POL, NSTAT>(U.stats + (size_t)step * 8, red, (float)ub.nrows);
+      if (U.stats && tid == 64) write_stats<POL, NSTAT, NW>(U.stats + (size_t)step * 8, red, (float)ub.nrows);
       return;
     }
 
@@ -454,7 +479,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     __syncthreads();                                     // #5
     STAMP(11);
     if (U.stats && tid == 64) {   // off the critical path: wave 1, after the exchange
-      write_stats<POL, NSTAT>(U.stats + (size_t)step * 8, red, (float)ub.nrows);
+      write_stats<POL, NSTAT, NW>(U.stats + (size_t)step * 8, red, (float)ub.nrows);
       gst(U.stats + (size_t)step * 8 + 6, red[80]);
       gst(U.stats + (size_t)step * 8 + 7, red[81]);
     }
@@ -463,7 +488,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     const float c1 = 1.f - H.b1, c2 = 1.f - H.b2;
 
     // ---- tf1 Adam on owned parameters (m, v in registers, weights in LDS) ----
-    // element (f = 16 fa + 4q + r, o = 16 w + c) sits at ebase[r] + 1024 fa in W1 / W2.
+    // element (f = 16 fa + 4q + r, o = 16 fo + c) sits at ebase[r] + 1024 fa in W1 / W2.
     // All owned weights are read first, then updated, then written (no read-after-write
     // ordering between different parameters' LDS words).
     {
@@ -472,7 +497,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       for (int i = 0; i < NTS; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          th[i][r] = (i < NS1 ? W.w2 : W.w1)[ebase[r] + 1024 * (i < NS1 ? i : i - NS1)];
+          th[i][r] = (i < NS1 ? W.w2 : W.w1)[ebase[r] + 1024 * tfa[i]];
 #pragma unroll
       for (int k = 0; k < NSLOT; ++k) {
         const int e = tid + NT * k;
@@ -501,7 +526,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
         for (int r = 0; r < 4; ++r) {
           const int f = 16 * tfa[i] + 4 * q + r;
           if (tv[i] && (i < NS1 || f < d))
-            (i < NS1 ? W.w2 : W.w1)[ebase[r] + 1024 * (i < NS1 ? i : i - NS1)] = th[i][r];
+            (i < NS1 ? W.w2 : W.w1)[ebase[r] + 1024 * tfa[i]] = th[i][r];
         }
 #pragma unroll
       for (int k = 0; k < NSLOT; ++k) {
@@ -554,23 +579,26 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 }
 
 template <int A, int KS1>
-__global__ void __launch_bounds__(NT) k_update_ffn(UpdateBatch ub) {
+__global__ void __launch_bounds__(64 * waves_for(A)) k_update_ffn(UpdateBatch ub) {
   extern __shared__ float lds[];
+  constexpr int NW = waves_for(A);
   const int p = blockIdx.x >> 1;
   const UpdateArgs U = ub.a[p];
-  if (blockIdx.x & 1) update_loop<A, KS1, 1, false>(U, ub, lds, p);
-  else update_loop<A, KS1, 2 * A, true>(U, ub, lds, p);
+  if (blockIdx.x & 1) update_loop<A, KS1, 1, false, NW>(U, ub, lds, p);
+  else update_loop<A, KS1, 2 * A, true, NW>(U, ub, lds, p);
 }
 
 // stride: the widest record stride of the launched policies (staging buffer rows)
 static size_t update_lds_bytes(int O, int stride) {
   const int nsb = 64 * O + O + 128;
-  return (size_t)(BRANCH_LDS_FLOATS + 2 * 64 * FM_LD + NW * nsb + 256 + DDRL_MB * 4 * stg_chunks(stride, O / 2)) * 4;
+  return (size_t)(BRANCH_LDS_FLOATS + 2 * 64 * FM_LD + waves_for(O / 2) * nsb + 256 +
+                  DDRL_MB * 4 * stg_chunks(stride, O / 2)) * 4;
 }
 
 template <int A, int KS1>
 static void launch_update_t(hipStream_t s, const UpdateBatch& ub, int P, int stride) {
-  hipLaunchKernelGGL((k_update_ffn<A, KS1>), dim3(2 * P), dim3(NT), update_lds_bytes(2 * A, stride), s, ub);
+  hipLaunchKernelGGL((k_update_ffn<A, KS1>), dim3(2 * P), dim3(64 * waves_for(A)), update_lds_bytes(2 * A, stride), s,
+                     ub);
 }
 
 void launch_update_ffn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHyper& h, int nrows, float inv_n,
