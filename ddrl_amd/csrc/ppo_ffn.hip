@@ -1,6 +1,6 @@
 // a13-a17: fused PPO minibatch SGD for the fcnet policy/value model (persistent kernel).
 //
-// Two workgroups per policy, on two CUs: blockIdx = 2p + branch, branch 0 = policy branch
+// Two workgroups per policy, on two CUs of one XCD: blockIdx = p + 8 branch, branch 0 = policy branch
 // (fc_1, fc_2, fc_out), branch 1 = value branch (fc_value_1, fc_value_2, value_out).  The
 // branches share no parameters, so each workgroup computes its own gradients and runs Adam
 // on its own parameters; the only coupling is tf.clip_by_global_norm, which needs the
@@ -179,7 +179,7 @@ __device__ __forceinline__ int perm_slot(const UpdateArgs& U, int step) {
 // Diagnostic build only (-DDDRL_STAMPS): per-phase s_memtime cycle counts of wave 0 of each
 // workgroup, accumulated over the steps of one launch; no stamp executes in the real build.
 #ifdef DDRL_STAMPS
-__device__ unsigned long long g_stamps[2 * DDRL_MAXP][16];
+__device__ unsigned long long g_stamps[16][16];
 #define STAMP_INIT unsigned long long st_prev = __builtin_amdgcn_s_memtime(), st_acc[16] = {0};
 #define STAMP(k) do { if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[k] += t_ - st_prev; st_prev = t_; } } while (0)
 #define STAMP_DONE do { if (tid == 0) for (int k_ = 0; k_ < 16; ++k_) g_stamps[blockIdx.x][k_] = st_acc[k_]; } while (0)
@@ -582,9 +582,13 @@ template <int A, int KS1>
 __global__ void __launch_bounds__(64 * waves_for(A)) k_update_ffn(UpdateBatch ub) {
   extern __shared__ float lds[];
   constexpr int NW = waves_for(A);
-  const int p = blockIdx.x >> 1;
+  // policy branch of policy p = block p, value branch = block p + 8: blocks b and b + 8 are
+  // dealt to the same XCD, so the per-step norm exchange stays inside one XCD (speed only;
+  // the exchange is agent-scope either way).  Blocks P..7 have no work.
+  const int p = blockIdx.x & 7;
+  if (p >= ub.h.P) return;
   const UpdateArgs U = ub.a[p];
-  if (blockIdx.x & 1) update_loop<A, KS1, 1, false, NW>(U, ub, lds, p);
+  if (blockIdx.x >> 3) update_loop<A, KS1, 1, false, NW>(U, ub, lds, p);
   else update_loop<A, KS1, 2 * A, true, NW>(U, ub, lds, p);
 }
 
@@ -597,7 +601,7 @@ static size_t update_lds_bytes(int O, int stride) {
 
 template <int A, int KS1>
 static void launch_update_t(hipStream_t s, const UpdateBatch& ub, int P, int stride) {
-  hipLaunchKernelGGL((k_update_ffn<A, KS1>), dim3(2 * P), dim3(64 * waves_for(A)), update_lds_bytes(2 * A, stride), s,
+  hipLaunchKernelGGL((k_update_ffn<A, KS1>), dim3(8 + P), dim3(64 * waves_for(A)), update_lds_bytes(2 * A, stride), s,
                      ub);
 }
 

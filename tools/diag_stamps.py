@@ -33,9 +33,9 @@ for it in range(2):
     ctx.ppo_update(0xF, sh, pe, [0.2] * 4)
     ctx.synchronize()
     dt = time.perf_counter() - t0
-st = (ctypes.c_ulonglong * (8 * 16))()
+st = (ctypes.c_ulonglong * (16 * 16))()
 assert N.load().ddrl_diag_stamps(st) == 0
-a = np.array(st, dtype=np.float64).reshape(8, 16)[:, :14] / steps
+a = np.array(st, dtype=np.float64).reshape(16, 16)[[0, 8], :14] / steps
 names = ["fwd", "loss", "dpp head/bias", "head bwd+db2+stores", "layer2 bwd+db1", "sync#1",
          "dW2 tiles", "sync#2", "X/dZ1 stores + sync#3", "prefetch issue", "dW1 tiles",
          "norm+exchange", "adam", "sync#6"]
