@@ -60,6 +60,16 @@ def ffn_fwd_flops_per_row(d, A, H=64):
     return 2 * (d * H + H * H + H * 2 * A + d * H + H * H + H)
 
 
+def gnn_flops_per_row(A, H=64, F=19):
+    """GraphNet actor + critic on one training row (a graph of 4 nodes): per net and node
+    the hypernetwork (4 x 1216), f W_n (19 x 64), message and node layers (64 x 64 each),
+    the selected node's head; backward = 2 x forward (input and weight gradients, the
+    hypernetwork recomputed counts once more)."""
+    fwd_net = lambda O: 2 * (4 * (4 * F * H + F * H + 2 * H * H) + H * O)
+    fwd = fwd_net(2 * A) + fwd_net(1)
+    return 3 * fwd + 2 * 4 * 4 * F * H * 2
+
+
 def cpu_baseline(env, n_envs=128, T=200, seed=0):
     """The numpy oracle on a bounded sample of the same workload (same env, same PPO
     schedule, fewer envs), BLAS limited to one thread.  Returns env-steps/s."""
@@ -128,6 +138,8 @@ def main():
     ap.add_argument("--frag", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-envs", type=int, default=512)
+    ap.add_argument("--ddp-mode", default="local", choices=["split", "local"],
+                    help="shared-policy envs on N>1 GPUs: per-rank rows per SGD step (see ddrl_amd/ddp.py)")
     args = ap.parse_args()
 
     import torch
@@ -154,11 +166,16 @@ def main():
     cfg, inst = make_cfg(args.env, n_local, T)
     stream = torch.cuda.current_stream()
     ctx = N.Context(cfg, local, stream.cuda_stream)
-    rng = np.random.default_rng(1234 + rank)
-    from ddrl_amd.trainer import glorot_ffn_flat
     P, A = cfg.n_policies, cfg.act_dim
+    gnn = cfg.model_kind == N.MODEL_GNN
+    # shared-policy envs on several GPUs train data-parallel (identical weights on every
+    # rank); independent-policy envs are replicas (own weights per rank)
+    ddp = world > 1 and P == 1
+    rng = np.random.default_rng(1234 if ddp else 1234 + rank)
+    from ddrl_amd.trainer import glorot_ffn_flat
+    from ddrl_amd.models import glorot_gnn_flat
     for p in range(P):
-        ctx.params_set(p, glorot_ffn_flat(rng, cfg.obs_dim[p], A))
+        ctx.params_set(p, glorot_gnn_flat(rng, A) if gnn else glorot_ffn_flat(rng, cfg.obs_dim[p], A))
     syn = SyntheticRollout(n_local, T, cfg.obs_full_dim, cfg.n_agents, A, f"cuda:{local}", seed=rank)
     kl = [0.2] * P
     R = [T * ctx.layout[p]["C"] for p in range(P)]
@@ -168,6 +185,14 @@ def main():
     gen.manual_seed(99 + rank)
     ev_upd = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     upd_ms = []
+    if ddp:
+        from ddrl_amd.ddp import Comm, DataParallelLearner, HipBackend, sync_filters, sync_standardize
+        comm = Comm(f"cuda:{local}")
+        learner = DataParallelLearner(HipBackend(ctx), comm, 0, 128, args.ddp_mode)
+        filter_base = ctx.filter_get()
+        ctx.filter_delta_reset()
+        grad = torch.zeros(ctx.n_params[0], dtype=torch.float32, device=f"cuda:{local}")
+        sched_rng = np.random.default_rng(77 + rank)
 
     ctx.observe(syn.obs[0])
 
@@ -179,6 +204,23 @@ def main():
             ctx.observe(syn.obs[t + 1])
         ctx.bootstrap()
         ctx.gae()
+        if ddp:
+            nonlocal filter_base
+            filter_base = sync_filters(comm, filter_base, ctx.filter_delta_get())
+            ctx.filter_set(*filter_base)
+            ctx.filter_delta_reset()
+            ctx.adv_norm_set(0, *sync_standardize(comm, ctx.adv_sums_get(0)))
+            sh, pe = learner.schedule(sched_rng, R[0], E)
+            sh_dev = torch.from_numpy(sh).to(stream.device)
+            ev_upd[0].record(stream)
+            mkl = learner.learn(sh_dev, pe, kl[0], grad)
+            ev_upd[1].record(stream)
+            kl[0] = kl[0] * 1.5 if mkl > 2 * 0.01 else (kl[0] * 0.5 if mkl < 0.5 * 0.01 else kl[0])
+            if record:
+                torch.cuda.synchronize()
+                upd_ms.append(ev_upd[0].elapsed_time(ev_upd[1]))
+                steps_done.append(pe.size)
+            return
         shuffles = [torch.randperm(R[p], device=stream.device, generator=gen, dtype=torch.int32) for p in range(P)]
         perms = [torch.stack([torch.randperm(nb[p], device=stream.device, generator=gen, dtype=torch.int32)
                               for _ in range(E)]).contiguous() for p in range(P)]
@@ -192,7 +234,9 @@ def main():
             kl[p] = kl[p] * 1.5 if mkl > 2 * 0.01 else (kl[p] * 0.5 if mkl < 0.5 * 0.01 else kl[p])
         if record:
             upd_ms.append(ev_upd[0].elapsed_time(ev_upd[1]))
+            steps_done.append(E * nb[0])
 
+    steps_done = []
     for _ in range(args.warmup):
         iteration(False)
     torch.cuda.synchronize()
@@ -218,18 +262,32 @@ def main():
         env_steps = int(es.item())
 
     upd_avg_ms = float(np.mean(upd_ms))
-    steps_per_policy = E * nb[0]
+    steps_per_policy = int(steps_done[-1])
     mb_latency_ms = upd_avg_ms / steps_per_policy                 # one policy's sequential step
     mb_amortized_ms = upd_avg_ms / (steps_per_policy * P)        # reference's learn_time / (P*10*nb)
     d = cfg.obs_dim[0]
-    flops_launch = ffn_flops_per_row(d, A) * 128 * steps_per_policy * P
+    rows_per_step = learner.rows_per_rank if ddp else 128
+    flops_row = gnn_flops_per_row(A) if gnn else ffn_flops_per_row(d, A)
+    flops_launch = flops_row * rows_per_step * steps_per_policy * P
     achieved_tf = flops_launch / (upd_avg_ms * 1e-3) / 1e12
-    # one launch keeps 2 workgroups (policy / value branch) per policy resident, one per CU:
-    # the per-CU fraction is the achieved rate over the MFMA peak of the CUs it occupies
-    active_cus = 2 * P
+    ks1 = (d + 3) // 4
+    if gnn:
+        kernel = "k_gnn<GRAD> + k_gnn_reduce + k_gnn_adam (three launches per minibatch step)"
+        active_cus = 2 * ((rows_per_step + 3) // 4)
+        model = f"shared GraphNet/MPNN leg policy (4 nodes x 19 features + ego quaternion, A={A})"
+    else:
+        kernel = (f"k_update_ffn<{A}, {ks1}> grad + RCCL all-reduce + k_apply_adam per step" if ddp else
+                  "k_update_ffn (fused PPO minibatch SGD, one launch per iteration)")
+        # the fused launch keeps 2 workgroups (policy / value branch) per policy, one per CU
+        active_cus = 2 * P
+        model = f"{P} {'shared' if P == 1 else 'independent'} fcnet 2x64 polic{'y' if P == 1 else 'ies'} (d={d}, A={A})"
     # algorithmic HBM bytes: each minibatch row's record fields read once per branch
     # (policy: obs, action, old logits, logp, adv; value: obs, vf, vt) + its shuffle index
-    rec_bytes_launch = 4 * (2 * d + 3 * A + 4 + 2) * 128 * steps_per_policy * P
+    obs_len = 93 if gnn else d
+    rec_bytes_launch = 4 * (2 * obs_len + 3 * A + 4 + 2) * rows_per_step * steps_per_policy * P
+    parallelism = (f"data-parallel over {world} ranks: RCCL all-reduce of the gradient every SGD step "
+                   f"({args.ddp_mode} mode, {rows_per_step} rows per rank per step)" if ddp else
+                   "replicas (no collective)")
     result = {
         "metric": METRIC,
         "value": env_steps / t_max,
@@ -244,26 +302,26 @@ def main():
         "dtype": "fp32",
         "data": "synthetic QuAntruped rollouts resident in HBM (no MuJoCo); Glorot-init weights",
         "config": {
-            "workload": f"{args.env}: {args.envs} envs x {cfg.n_agents} leg agents, {P} independent "
-                        f"fcnet 2x64 policies (d={d}, A={A}), T={T}, train batch {R[0]} rows/policy, "
-                        f"{E} epochs x {nb[0]} minibatches x 128",
-            "envs_total": args.envs, "envs_per_gpu": n_local, "parallelism": "replicas (no collective)",
+            "workload": f"{args.env}: {args.envs} envs x {cfg.n_agents} leg agents, {model}, T={T}, "
+                        f"train batch {R[0]} rows/policy/rank, {E} epochs x {steps_per_policy // E} "
+                        f"minibatches x {rows_per_step} rows",
+            "envs_total": args.envs, "envs_per_gpu": n_local, "parallelism": parallelism,
         },
         "ppo_update_ms_per_minibatch": mb_amortized_ms,
         "ppo_update_ms_per_minibatch_latency": mb_latency_ms,
         "update_kernel_ms": upd_avg_ms,
         "roofline": {
-            "kernel": "k_update_ffn (fused PPO minibatch SGD, one launch per iteration)",
+            "kernel": kernel,
             "bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved_tf / PEAK_FP32_TFLOPS,
-            "traffic": pmc_traffic(f"k_update_ffn<{A}, ", steps_per_policy * P),
+            "traffic": None if (gnn or ddp) else pmc_traffic(f"k_update_ffn<{A}, {ks1}>", steps_per_policy * P),
             "algorithmic_flops_per_launch": flops_launch,
             "algorithmic_bytes_per_launch": rec_bytes_launch,
             "active_cus": active_cus,
             "frac_of_active_cus": achieved_tf / (PEAK_FP32_TFLOPS * active_cus / 256),
         },
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not gnn:
         v, dt, sample = cpu_baseline(args.env, args.cpu_envs, T)
         result["cpu_baseline"] = {"value": v, "unit": "env-steps/s", "cores": 1, "kind": "port",
                                   "sample": sample + f"; {dt:.1f} s", "host_cpus": os.cpu_count()}

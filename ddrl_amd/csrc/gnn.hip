@@ -433,26 +433,29 @@ __global__ void __launch_bounds__(256) k_gnn_reduce(GnnArgs ga, int ntiles, int 
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
   __syncthreads();
   if (threadIdx.x == 0) ga.normp[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
-  if (blockIdx.x == 0 && threadIdx.x == 64) {
-    // loss statistics of the step: statp [tile][8] per net (actor block then critic block)
+  if (blockIdx.x == 0 && threadIdx.x >= 64 && threadIdx.x < 64 + 10) {
+    // loss statistics of the step: statp [net][tile][8]; lane j of wave 1 sums (net, stat)
+    // j over the tiles (independent loads), lane 64 combines
+    __shared__ float sv[10];
+    const int j = threadIdx.x - 64, b = j / 5, k = j - 5 * b;
+    float a = 0.f;
+    for (int t = 0; t < ntiles; ++t) a += ga.statp[(b * DDRL_MB / 4 + t) * 8 + k];
+    sv[j] = a;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     const UpdateArgs& U = ga.u;
-    ga.bp_cur[0] = U.beta_pow[0];
-    ga.bp_cur[1] = U.beta_pow[1];
-    if (U.stats) {
-      float sv[2][5];
-      for (int b = 0; b < 2; ++b)
-        for (int k = 0; k < 5; ++k) {
-          float a = 0.f;
-          for (int t = 0; t < ntiles; ++t) a += ga.statp[(b * DDRL_MB / 4 + t) * 8 + k];
-          sv[b][k] = a;
-        }
-      const float nr = (float)ga.n_graphs;
-      float* so = U.stats + (size_t)ga.step * 8;
-      so[1] = sv[0][0] / nr; so[3] = sv[0][1] / nr; so[4] = sv[0][2] / nr;
-      so[2] = sv[1][0] / nr;
-      const float vy = sv[1][2] / nr - (sv[1][1] / nr) * (sv[1][1] / nr);
-      const float vd = sv[1][4] / nr - (sv[1][3] / nr) * (sv[1][3] / nr);
-      so[5] = vy > 0.f ? fmaxf(-1.f, 1.f - vd / vy) : 0.f;
+    if (j == 0) {
+      ga.bp_cur[0] = U.beta_pow[0];
+      ga.bp_cur[1] = U.beta_pow[1];
+      if (U.stats) {
+        const float nr = (float)ga.n_graphs;
+        float* so = U.stats + (size_t)ga.step * 8;
+        so[1] = sv[0] / nr; so[3] = sv[1] / nr; so[4] = sv[2] / nr;
+        so[2] = sv[5] / nr;
+        const float vy = sv[7] / nr - (sv[6] / nr) * (sv[6] / nr);
+        const float vd = sv[9] / nr - (sv[8] / nr) * (sv[8] / nr);
+        so[5] = vy > 0.f ? fmaxf(-1.f, 1.f - vd / vy) : 0.f;
+      }
     }
   }
 }
@@ -462,9 +465,12 @@ __global__ void __launch_bounds__(256) k_gnn_adam(GnnArgs ga, int nred, int n) {
   __shared__ float scale_s;
   const UpdateArgs& U = ga.u;
   const UpdateHyper& h = ga.h;
-  if (threadIdx.x == 0) {
-    float tot = 0.f;
-    for (int b = 0; b < nred; ++b) tot += ga.normp[b];
+  if (threadIdx.x < 64) {
+    // squared-norm partials of the reduction blocks: the same butterfly in every block
+    float part = 0.f;
+    for (int b = threadIdx.x; b < nred; b += 64) part += ga.normp[b];
+    const float tot = wave_sum(part);
+    if (threadIdx.x != 0) goto done;
     const float gn = sqrtf(tot);
     scale_s = h.grad_clip * fminf(1.f / gn, 1.f / h.grad_clip);
     if (blockIdx.x == 0) {
@@ -476,6 +482,7 @@ __global__ void __launch_bounds__(256) k_gnn_adam(GnnArgs ga, int nred, int n) {
       U.beta_pow[1] = ga.bp_cur[1] * h.b2;
     }
   }
+done:
   __syncthreads();
   const int p = blockIdx.x * 256 + threadIdx.x;
   if (p >= n) return;
