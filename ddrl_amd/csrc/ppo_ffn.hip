@@ -96,13 +96,16 @@ struct RowData {
 // per-lane dword gathers: 3 line requests per row rather than one per field and lane.
 // The staging rows hold cpr_l = cpr | 1 chunks (an odd number: the 16 rows a lane group
 // reads then start in 16 different banks); the pad chunk repeats the row's last chunk.
-template <int NT>
+// Issued by waves 0 .. NW-2: the last wave keeps its vector-memory counter free for the
+// norm exchange (an early partner poll would otherwise wait for the gathers too).
+template <int NW>
 __device__ __forceinline__ void issue_rows(const float* rec, int stride, int cpr, int cpr_l, const int* idxb,
                                            float* stg) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (w == NW - 1) return;
   const int nchunk = DDRL_MB * cpr_l;
   const float inv = 1.f / (float)cpr_l;
-  for (int base = 64 * w; base < nchunk; base += NT) {   // wave-uniform
+  for (int base = 64 * w; base < nchunk; base += 64 * (NW - 1)) {   // wave-uniform
     const int g = base + lane;
     const int row = (int)(((float)g + 0.5f) * inv);
     const int k = min(g - row * cpr_l, cpr - 1);
@@ -273,7 +276,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   const int tr = tid < ub.nrows ? tid : 0;
   if (tid < DDRL_MB) idxb[tid] = U.step0 < last && tid < ub.nrows ? row_index(U, U.step0, tr, true) : 0;
   __syncthreads();
-  if (U.step0 < last) issue_rows<NT>(U.rec, stride, cpr, cpr_l, idxb, stg);
+  if (U.step0 < last) issue_rows<NW>(U.rec, stride, cpr, cpr_l, idxb, stg);
   wait_vmcnt0();
   __syncthreads();
   if (tid < DDRL_MB) idxb[tid] = U.step0 + 1 < last && tid < ub.nrows ? row_index(U, U.step0 + 1, tr, true) : 0;
@@ -308,6 +311,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     // of the 16 features (fb, r) a lane holds; afterwards lane (c, q) owns feature
     // h = 16 (c >> 2) + 4 q + (c & 3).
     const int h_own = 16 * (c >> 2) + 4 * q + (c & 3);
+#ifndef DDRL_ABL_NO_HEADDPP
 #pragma unroll
     for (int o = 0; o < OB; ++o) {
       float v[16];
@@ -321,6 +325,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
         }
       Pw[h_own * OB + o] = row16_transpose_sum(v);
     }
+#endif
 #pragma unroll
     for (int o = 0; o < OB; ++o) {
       float dsum = dout[0][o];
@@ -358,7 +363,9 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       store_act_fm(bufB, RT * w + t, dz[t]);
     }
     STAMP(3);
+#ifndef DDRL_ABL_NO_L2BWD
     layer2_bwd_rt<RT>(W, dz, h2);                        // h2 <- dH1
+#endif
 #pragma unroll
     for (int t = 0; t < RT; ++t) dtanh_inplace(h2[t], h1[t]);  // h2 = dZ1
     {
@@ -377,7 +384,11 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     __syncthreads();                                     // #1: H1, dZ2, partials visible
     STAMP(5);
     floatx4 gt[NTS];
+#ifndef DDRL_ABL_NO_DW2   // ablation builds (timing only): skip a phase
     dw_tiles_fm<DDRL_MB, NS1>(bufA, bufB, tfa, w & 3, gt);   // dW2 tiles of this wave
+#else
+    for (int i = 0; i < NS1; ++i) gt[i] = splat4(0.f);
+#endif
     STAMP(6);
     __syncthreads();                                     // #2: dW2 operands consumed
     STAMP(7);
@@ -391,7 +402,16 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     STAMP(8);
     // ---- prefetch: the records of step + 1 land in stg (LDS-DMA) while the dW1 tiles, the
     //      norm exchange and Adam run; every lane has read its rows of this step (sync #1)
-    if (step + 1 < last) issue_rows<NT>(U.rec, stride, cpr, cpr_l, idxb, stg);
+#ifndef DDRL_ABL_NO_PREFETCH
+    if (step + 1 < last) issue_rows<NW>(U.rec, stride, cpr, cpr_l, idxb, stg);
+#endif
+    // the exchange lane (wave NW-1, which issued no gathers) polls the partner's granule
+    // early: when the other branch is ahead, its norm^2 is already there at the exchange
+    const int xlane = 64 * (NW - 1);
+    unsigned long long* const xmine = ub.xchg + ((size_t)p * 2 + (POL ? 0 : 1)) * 2 + (step & 1);
+    unsigned long long* const xother = ub.xchg + ((size_t)p * 2 + (POL ? 1 : 0)) * 2 + (step & 1);
+    unsigned long long xv = 0;
+    if (tid == xlane) xv = __hip_atomic_load(xother, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     STAMP(9);
     {
       // dW1 tiles of this wave: the valid slots are a prefix (tiles w + NW i < 4 nf1)
@@ -400,6 +420,9 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       int n1 = 0;
 #pragma unroll
       for (int i = NS1; i < NTS; ++i) n1 += tv[i] ? 1 : 0;
+#ifdef DDRL_ABL_NO_DW1
+      n1 = -1;
+#endif
       if (n1 == NS2) dw_tiles_fm<DDRL_MB, NS2>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
       else if constexpr (NS2 >= 3) {
         if (n1 == 2) dw_tiles_fm<DDRL_MB, 2>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
@@ -451,18 +474,19 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     ss = wave_sum(ss);
     if (lane == 0) red[64 + w] = ss;
     __syncthreads();                                     // #4
-    if (tid == 0) {
+    if (tid == xlane) {
       float local = 0.f;
       for (int i = 0; i < NW; ++i) local += red[64 + i];
       const unsigned tag = (unsigned)step + 1u;
-      unsigned long long* mine = ub.xchg + ((size_t)p * 2 + (POL ? 0 : 1)) * 2 + (step & 1);
-      unsigned long long* other = ub.xchg + ((size_t)p * 2 + (POL ? 1 : 0)) * 2 + (step & 1);
-      __hip_atomic_store(mine, ((unsigned long long)tag << 32) | __float_as_uint(local),
+      __hip_atomic_store(xmine, ((unsigned long long)tag << 32) | __float_as_uint(local),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      unsigned long long v;
+      unsigned long long v = xv;
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-      while (true) {
-        v = __hip_atomic_load(other, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef DDRL_ABL_NO_EXCHANGE
+      v = ((unsigned long long)tag << 32) | __float_as_uint(local);
+#endif
+      while ((unsigned)(v >> 32) != tag) {
+        v = __hip_atomic_load(xother, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if ((unsigned)(v >> 32) == tag) break;
         if (__builtin_amdgcn_s_memrealtime() - t0 > 300000000ull) {   // 3 s at 100 MHz
           atomicExch(ub.err, 1);
@@ -487,6 +511,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     const float alpha = H.lr * sqrtf(1.f - b2p) / (1.f - b1p);
     const float c1 = 1.f - H.b1, c2 = 1.f - H.b2;
 
+#ifndef DDRL_ABL_NO_ADAM
     // ---- tf1 Adam on owned parameters (m, v in registers, weights in LDS) ----
     // element (f = 16 fa + 4q + r, o = 16 fo + c) sits at ebase[r] + 1024 fa in W1 / W2.
     // All owned weights are read first, then updated, then written (no read-after-write
@@ -534,6 +559,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
         if (e < NSB) { int pidx; float* lp; small_param<OB>(e, bo, W, pidx, lp); *lp = ts[k]; }
       }
     }
+#endif
     b1p = b1p * H.b1;
     b2p = b2p * H.b2;
     STAMP(12);

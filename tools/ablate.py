@@ -1,0 +1,70 @@
+"""Ablation timing of the fused update kernel: builds diagnostic variants that each skip
+one phase (results are wrong; only the per-step time matters) and reports us/step.
+
+    python tools/ablate.py build        # in the container (hipcc)
+    python tools/ablate.py run [envs]   # on the GPU box
+"""
+import os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+VARIANTS = ["", "DDRL_ABL_NO_DW2", "DDRL_ABL_NO_DW1", "DDRL_ABL_NO_L2BWD", "DDRL_ABL_NO_PREFETCH",
+            "DDRL_ABL_NO_ADAM", "DDRL_ABL_NO_EXCHANGE", "DDRL_ABL_NO_HEADDPP", "DDRL_ABL_NO_TANH"]
+
+
+def paths(v):
+    from ddrl_amd import native as N
+    d = os.path.dirname(N.LIB_PATH)
+    tag = v.replace("DDRL_ABL_", "").lower() or "base"
+    return os.path.join(d, f"libddrl_hip_abl_{tag}.so"), os.path.join(d, f"_build_abl_{tag}")
+
+
+def build():
+    from ddrl_amd import build as B
+    for v in VARIANTS:
+        lib, bd = paths(v)
+        print(B.build(extra_flags=[f"-D{v}"] if v else [], lib=lib, build_dir=bd), flush=True)
+
+
+def run(n):
+    import subprocess
+    for v in VARIANTS:
+        lib, _ = paths(v)
+        out = subprocess.run([sys.executable, __file__, "one", lib, str(n)], capture_output=True, text=True)
+        print(f"{v or 'baseline':28s} {out.stdout.strip()} {out.stderr.strip()[-200:]}", flush=True)
+
+
+def one(lib, n):
+    import numpy as np, torch
+    from ddrl_amd import native as N
+    N.load(lib)
+    from ddrl_amd.spec import make_cfg
+    from ddrl_amd.trainer import glorot_ffn_flat
+    T = 200
+    cfg, _ = make_cfg("QuantrupedMultiEnv_Local", n, T)
+    ctx = N.Context(cfg, 0, torch.cuda.current_stream().cuda_stream)
+    rng = np.random.default_rng(0)
+    for p in range(4):
+        ctx.params_set(p, glorot_ffn_flat(rng, 35, 2))
+        lay = ctx.layout[p]
+        r = rng.normal(size=(T * lay["C"], lay["stride"])).astype(np.float32) * 0.5
+        ctx.records_set(p, r)
+    R = T * n
+    nb = R // 128
+    sh = [torch.from_numpy(rng.permutation(R).astype(np.int32)).cuda() for _ in range(4)]
+    pe = [torch.from_numpy(np.stack([rng.permutation(nb) for _ in range(10)]).astype(np.int32)).cuda()
+          for _ in range(4)]
+    best = 1e9
+    for _ in range(3):
+        t0 = time.perf_counter()
+        ctx.ppo_update(0xF, sh, pe, [0.2] * 4)
+        ctx.synchronize()
+        best = min(best, time.perf_counter() - t0)
+    print(f"{best / (10 * nb) * 1e6:.2f} us/step")
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "build":
+        build()
+    elif sys.argv[1] == "run":
+        run(int(sys.argv[2]) if len(sys.argv) > 2 else 512)
+    else:
+        one(sys.argv[2], int(sys.argv[3]))
