@@ -100,6 +100,9 @@ def load(path: str = LIB_PATH):
     if not os.path.exists(path):
         raise DdrlError(f"{path} is missing: build it with `python -m ddrl_amd.build` "
                         "(the HIP library is the only compute path; there is no fallback)")
+    # torch ships its own libamdhip64.so.7 (same soname as /opt/rocm's): import it first so
+    # this library binds to the process's single HIP runtime instead of starting a second one
+    import torch  # noqa: F401
     lib = C.CDLL(path)
     for name, (args, res) in _SIGS.items():
         fn = getattr(lib, name)
