@@ -115,7 +115,9 @@ static int validate(const ddrl_cfg& c) {
   for (int j = 0; j < c.n_agents; ++j) {
     const int d = c.obs_dim[c.agent_policy[j]];
     for (int f = 0; f < d; ++f)
-      if (c.obs_index[j][f] < 0 || c.obs_index[j][f] >= c.obs_full_dim) return fail("bad obs_index");
+      if (c.obs_index[j][f] < -2 || c.obs_index[j][f] >= c.obs_full_dim ||
+          (c.model_kind == DDRL_MODEL_GNN && c.obs_index[j][f] < 0))
+        return fail("bad obs_index");
     if (c.n_contact[j] < 0 || c.n_contact[j] > 14) return fail("bad n_contact");
     for (int b = 0; b < c.n_contact[j]; ++b)
       if (c.contact_index[j][b] < 0 || c.contact_index[j][b] >= 14) return fail("bad contact_index");
@@ -163,7 +165,11 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
     for (int s = 0; s < P.k; ++s) {
       pr.agent[s] = P.agents[s];
       for (int f = 0; f < DDRL_MAXD; ++f) pr.obs_index[s][f] = g.obs_index[P.agents[s]][f];
-      for (int a = 0; a < 8; ++a) pr.act_index[s][a] = g.act_index[P.agents[s]][a];
+      pr.act_neg[s] = 0;
+      for (int a = 0; a < 8; ++a) {
+        pr.act_index[s][a] = g.act_index[P.agents[s]][a];
+        if (g.act_negate[P.agents[s]][a]) pr.act_neg[s] |= 1 << a;
+      }
     }
     const size_t stage_n = g.model_kind == DDRL_MODEL_GNN ? (size_t)N * 4 * 23 : (size_t)P.C * P.d;
     rc = rc || dalloc(c, &P.theta, P.n_params) || dalloc(c, &P.m, P.n_params) ||

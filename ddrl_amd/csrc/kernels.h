@@ -25,6 +25,7 @@ struct PolicyRoute {
   int agent[DDRL_MAXAG];    // agent id of each slot
   int obs_index[DDRL_MAXAG][DDRL_MAXD];
   int act_index[DDRL_MAXAG][8];
+  int act_neg[DDRL_MAXAG];         // bit j: negate action j in the env vector (LegTransforms)
 };
 
 struct RouteArgs {

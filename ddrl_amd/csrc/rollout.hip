@@ -98,7 +98,8 @@ __global__ void k_observe_ffn(RouteArgs ra, const float* __restrict__ obs,
   const int c = gid / pr.d, f = gid - c * pr.d;
   const int e = c / pr.k, slot = c - e * pr.k;
   const int idx = pr.obs_index[slot][f];
-  stage_tab[p][(size_t)c * pr.d + f] = norm_obs(obs[(size_t)e * ra.full_dim + idx], normc, idx, clip);
+  stage_tab[p][(size_t)c * pr.d + f] =
+      idx >= 0 ? norm_obs(obs[(size_t)e * ra.full_dim + idx], normc, idx, clip) : (idx == -2 ? 1.f : 0.f);
 }
 
 void launch_observe_ffn(hipStream_t s, const RouteArgs& ra, const float* obs, const double* normc,
@@ -202,7 +203,8 @@ __global__ void __launch_bounds__(256) k_act_ffn(RouteArgs ra, ActArgs aa) {
 #pragma unroll
     for (int j = 0; j < A; ++j) {
       rp[L.act + j] = act[j];
-      aa.actions[(size_t)e * 8 + pr.act_index[slot][j]] = fminf(fmaxf(act[j], -1.f), 1.f);
+      const float ac = fminf(fmaxf(act[j], -1.f), 1.f);
+      aa.actions[(size_t)e * 8 + pr.act_index[slot][j]] = (pr.act_neg[slot] >> j) & 1 ? -ac : ac;
     }
   } else if (q == 1) {
 #pragma unroll

@@ -38,6 +38,7 @@ class DdrlCfg(C.Structure):
         ("vf_loss_coeff", f32), ("entropy_coeff", f32), ("lr", f32), ("grad_clip", f32),
         ("adam_beta1", f32), ("adam_beta2", f32), ("adam_eps", f32),
         ("vf_clip_mode", i32), ("sgd_minibatch_size", i32), ("num_sgd_iter", i32),
+        ("act_negate", (i32 * 8) * MAX_AG),
     ]
 
 

@@ -177,6 +177,38 @@ class QuantrupedSingleDecentralizedEnv(QuantrupedSingleControllerSuperEnv):
     pass
 
 
+class QuantrupedSingleDecentralizedLegIDEnv(QuantrupedSingleControllerSuperEnv):
+    """quantruped_singleDecentralizedController_environments.py:66-114: every agent
+    receives (leg index, 19 normalized features).  RLlib's Tuple preprocessor one-hot
+    encodes the MultiDiscrete part, so the model input is one_hot(index, 4) ++ features
+    (d = 23): `policy_obs_indices` encodes the one-hot as the constants -1 (0.0) and -2
+    (1.0) of the gather table."""
+    leg_angles = {'agent_FL': 45., 'agent_HL': 135., 'agent_HR': -135., 'agent_FR': -45.}
+
+    def _init_tables(self):
+        super()._init_tables()
+        self.policy_obs_indices = {a: [-2 if k == j else -1 for k in range(4)] + list(self.obs_indices[a])
+                                   for j, a in enumerate(self.agent_names)}
+
+    @staticmethod
+    def return_policies(use_target_velocity=False):
+        obs = Box(-float("inf"), float("inf"), (19 + use_target_velocity,), "float64")
+        space = Tuple([MultiDiscrete([4]), obs])
+        return {QuantrupedSingleControllerSuperEnv.policy_names[0]: (None, space, Box(-1.0, 1.0, (2,)), {})}
+
+
+class QuantrupedSingleDecentralizedLegTransforms(QuantrupedSingleControllerSuperEnv):
+    """quantruped_singleDecentralizedController_environments.py:117-148: the observation
+    scale is all ones (no-op); concatenate_actions negates the fr_knee and hr_knee actions
+    of the env action vector (`action_negate`).  Rewards use the agents' own actions, whose
+    squares the sign does not change."""
+
+    def _init_tables(self):
+        super()._init_tables()
+        neg = set(get_action_indices(['fr_knee']) + get_action_indices(['hr_knee']))
+        self.action_negate = {a: [i in neg for i in self.action_indices[a]] for a in self.agent_names}
+
+
 class QuantrupedTwoControllerSuperEnv(QuantrupedMultiPoliciesEnv):
     """quantruped_twoDecentralizedController_environments.py (A = 4, d = 27)."""
     groups = (('fl', 'hl'), ('hr', 'fr'))
@@ -270,6 +302,14 @@ class QuantrupedDecentralizedSharedGraphEnv(QuantrupedMultiPoliciesEnv):
         return {"leg_policy": (None, space, Box(-1.0, 1.0, (2,)), {})}
 
 
+class QuantrupedDecentralizedGraphEnv(QuantrupedFourControllerSuperEnv):
+    """quantruped_GraphDecentralizedController_environments.py:37-121: four policies with
+    19-d graph nodes.  The GraphNet ("gnn") needs 23-d nodes (19 features + the ego
+    quaternion of its hypernetwork), so this env has no consistent model pairing in the
+    reference; it is registered and refuses to build a context."""
+    model_kind = "gnn-19"
+
+
 # register_env names (simulation_envs/__init__.py:53-67).  The reference registers
 # "QuantrupedMultiEnv_Centralized" to the base class (Appendix B.2); it maps to the
 # working centralized env here.
@@ -285,6 +325,9 @@ ENV_REGISTRY = {
     "QuantrupedMultiEnv_TwoSides": Quantruped_TwoSideControllers_Env,
     "QuantrupedMultiEnv_TwoDiags": Quantruped_TwoDiagControllers_Env,
     "QuantrupedMultiEnv_SharedDecentral": QuantrupedSingleDecentralizedEnv,
+    "QuantrupedMultiEnv_SharedDecentralLegID": QuantrupedSingleDecentralizedLegIDEnv,
+    "QuantrupedMultiEnv_SharedDecentralLegTransforms": QuantrupedSingleDecentralizedLegTransforms,
+    "QuantrupedMultiEnv_Decentral_Graph": QuantrupedDecentralizedGraphEnv,
 }
 
 

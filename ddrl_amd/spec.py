@@ -30,6 +30,9 @@ def make_cfg(env, n_envs, frag_len=None, config=None):
     if isinstance(env, str):
         env = get_env_class(env)
     inst = env(env_config) if isinstance(env, type) else env
+    if inst.model_kind not in ("ffn", "gnn"):
+        raise ValueError(f"{type(inst).__name__}: no model of the reference fits this env's observations "
+                         "(SURVEY Appendix B.8)")
     agents = list(inst.agent_names)
     policies = list(type(inst).policy_names)
     mapping = type(inst).policy_mapping_fn
@@ -44,12 +47,13 @@ def make_cfg(env, n_envs, frag_len=None, config=None):
     for j, a in enumerate(agents):
         p = policies.index(mapping(a))
         c.agent_policy[j] = p
-        idx = inst.obs_indices[a]
+        idx = getattr(inst, "policy_obs_indices", inst.obs_indices)[a]   # model input columns
         c.obs_dim[p] = len(idx)
         for f, i in enumerate(idx):
             c.obs_index[j][f] = i
         for k, i in enumerate(inst.action_indices[a]):
             c.act_index[j][k] = i
+            c.act_negate[j][k] = int(getattr(inst, "action_negate", {}).get(a, [False] * 8)[k])
         ci, cw = inst.contact_force_indices[a]
         c.n_contact[j] = len(ci)
         for k, (i, w) in enumerate(zip(ci, cw)):

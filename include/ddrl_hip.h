@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define DDRL_ABI_VERSION 1
+#define DDRL_ABI_VERSION 2
 #define DDRL_MAX_POLICIES 4
 #define DDRL_MAX_AGENTS 4
 #define DDRL_MAX_OBS 48
@@ -50,7 +50,9 @@ typedef struct ddrl_cfg {
   int32_t act_dim;       /* A: actions per agent (2, 4 or 8)                               */
   int32_t agent_policy[DDRL_MAX_AGENTS];           /* policy id of every agent            */
   int32_t obs_dim[DDRL_MAX_POLICIES];              /* d per policy (GNN: 19 per node)      */
-  int32_t obs_index[DDRL_MAX_AGENTS][DDRL_MAX_OBS];/* gather table per agent (a1)          */
+  int32_t obs_index[DDRL_MAX_AGENTS][DDRL_MAX_OBS];/* gather table per agent (a1); entries
+                                                      -1 / -2 are the constants 0 / 1 (the
+                                                      one-hot leg id of the LegID env)      */
   int32_t act_index[DDRL_MAX_AGENTS][8];           /* scatter table per agent (a7)         */
   int32_t n_contact[DDRL_MAX_AGENTS];              /* contact-cost bodies per agent (a8)   */
   int32_t contact_index[DDRL_MAX_AGENTS][14];
@@ -69,6 +71,8 @@ typedef struct ddrl_cfg {
   int32_t vf_clip_mode;     /* DDRL_VF_CLIP_*                                               */
   int32_t sgd_minibatch_size;  /* 128 (the fused update kernel is built for 128)          */
   int32_t num_sgd_iter;        /* 10                                                       */
+  int32_t act_negate[DDRL_MAX_AGENTS][8];  /* 1: negate action j of the agent in the env action
+                                              vector (LegTransforms: fr / hr knee)          */
 } ddrl_cfg;
 
 typedef struct ddrl_ctx ddrl_ctx;

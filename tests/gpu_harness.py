@@ -66,8 +66,12 @@ class OracleRollout:
     def observe(self, obs):
         normed = O.mean_std_filter(obs, self.rs, update=True, clip=self.cfg.filter_clip)
         self.stage = []
+        tables = getattr(self.inst, "policy_obs_indices", self.inst.obs_indices)
+        # gather columns; the constants -1 / -2 (LegID one-hot) become 0 / 1
+        ext = np.concatenate([normed, np.zeros((normed.shape[0], 1)), np.ones((normed.shape[0], 1))], 1)
+        col = lambda i: i if i >= 0 else normed.shape[1] + (-1 - i)
         for p in range(self.cfg.n_policies):
-            cols = [normed[:, self.inst.obs_indices[a]] for a in self.slots[p]]
+            cols = [ext[:, [col(i) for i in tables[a]]] for a in self.slots[p]]
             x = np.stack(cols, 1).reshape(-1, self.cfg.obs_dim[p])   # c = e * k + slot
             self.stage.append(x.astype(np.float32))
 
@@ -86,7 +90,8 @@ class OracleRollout:
             r["obs"][t], r["act"][t], r["logits"][t] = x, a, logits
             r["logp"][t], r["vf"][t] = O.dg_logp(logits, a), value
             for s, name in enumerate(self.slots[p]):
-                actions[:, self.inst.action_indices[name]] = np.clip(a.reshape(-1, k, A)[:, s], -1, 1)
+                sign = np.where(getattr(self.inst, "action_negate", {}).get(name, [False] * A), -1.0, 1.0)
+                actions[:, self.inst.action_indices[name]] = np.clip(a.reshape(-1, k, A)[:, s], -1, 1) * sign
         return actions
 
     def reward(self, t, fw, cfrc, actions, done):

@@ -43,6 +43,8 @@ ROLLOUT_ENVS = [
     ("QuantrupedMultiEnv_SharedDecentral", 33, 5),
     ("QuantrupedMultiEnv_Centralized", 50, 4),
     ("QuantrupedMultiEnv_TwoSides", 20, 4),
+    ("QuantrupedMultiEnv_SharedDecentralLegID", 24, 4),
+    ("QuantrupedMultiEnv_SharedDecentralLegTransforms", 24, 4),
 ]
 
 
@@ -93,6 +95,7 @@ def _params_close(got, ref, lr, steps, msg):
     ("QuantrupedMultiEnv_Local", 64, 6, 3),
     ("QuantrupedMultiEnv_SharedDecentral", 32, 4, 2),
     ("QuantrupedMultiEnv_Centralized", 48, 8, 2),
+    ("QuantrupedMultiEnv_SharedDecentralLegID", 32, 4, 2),
 ])
 def test_ppo_update_parity(env, n, T, steps):
     import torch
