@@ -52,6 +52,8 @@ struct ddrl_ctx {
   RouteArgs route{};
   double *f_n = nullptr, *f_M = nullptr, *f_S = nullptr, *f_normc = nullptr;
   double *f_dn = nullptr, *f_dM = nullptr, *f_dS = nullptr;   // pushes since the last sync
+  double* pf = nullptr;   // per-policy RLlib MeanStdFilter state [P][PF_STRIDE]
+  double* zs = nullptr;   // fp64 column sums of the env-normalized observation [2][D]
   uint8_t* done_tn = nullptr;
   float** stage_tab = nullptr;    // device array of per-policy stage pointers
   int32_t* zero_perm = nullptr;
@@ -112,12 +114,16 @@ static int validate(const ddrl_cfg& c) {
   if (c.model_kind == DDRL_MODEL_GNN && (c.n_policies != 1 || c.n_agents != 4 || c.obs_dim[0] != 19))
     return fail("gnn requires one shared leg policy, 4 agents and 19 features per node");
   if (c.model_kind == DDRL_MODEL_GNN && c.act_dim != 2) return fail("gnn kernels are built for act_dim 2");
+  if (c.policy_filter && c.model_kind != DDRL_MODEL_FFN)
+    return fail("the per-policy MeanStdFilter is built for fcnet policies (flat observations)");
   for (int j = 0; j < c.n_agents; ++j) {
     const int d = c.obs_dim[c.agent_policy[j]];
     for (int f = 0; f < d; ++f)
       if (c.obs_index[j][f] < -2 || c.obs_index[j][f] >= c.obs_full_dim ||
           (c.model_kind == DDRL_MODEL_GNN && c.obs_index[j][f] < 0))
         return fail("bad obs_index");
+      else if (c.policy_filter && c.obs_index[j][f] < 0)
+        return fail("constant input columns (LegID) with the per-policy MeanStdFilter are not supported");
     if (c.n_contact[j] < 0 || c.n_contact[j] > 14) return fail("bad n_contact");
     for (int b = 0; b < c.n_contact[j]; ++b)
       if (c.contact_index[j][b] < 0 || c.contact_index[j][b] >= 14) return fail("bad contact_index");
@@ -187,7 +193,8 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
   }
   rc = rc || dalloc(c, &c->f_n, 1) || dalloc(c, &c->f_M, DDRL_MAXFULL) || dalloc(c, &c->f_S, DDRL_MAXFULL) ||
        dalloc(c, &c->f_normc, 2 * DDRL_MAXFULL) || dalloc(c, &c->f_dn, 1) ||
-       dalloc(c, &c->f_dM, DDRL_MAXFULL) || dalloc(c, &c->f_dS, DDRL_MAXFULL) || dalloc(c, &c->done_tn, (size_t)T * N) ||
+       dalloc(c, &c->f_dM, DDRL_MAXFULL) || dalloc(c, &c->f_dS, DDRL_MAXFULL) ||
+       dalloc(c, &c->pf, (size_t)DDRL_MAXP * PF_STRIDE) || dalloc(c, &c->zs, 2 * DDRL_MAXFULL) || dalloc(c, &c->done_tn, (size_t)T * N) ||
        dalloc(c, &c->stage_tab, DDRL_MAXP) || dalloc(c, &c->zero_perm, 4) ||
        dalloc(c, &c->d_uargs, DDRL_MAXP) || dalloc(c, &c->xchg, 4 * DDRL_MAXP) || dalloc(c, &c->err, 1) ||
        dalloc(c, &c->h_obs, (size_t)N * g.obs_full_dim) ||
@@ -344,6 +351,43 @@ int ddrl_filter_delta_reset(ddrl_ctx* c) {
   return 0;
 }
 
+static int pf_io(ddrl_ctx* c, int pid, double* n, double* M, double* S, bool set, bool delta) {
+  CHK_CTX(c);
+  if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
+  if (!n || !M || !S) return fail("null filter buffer");
+  const int d = c->pol[pid].d;
+  double* P = c->pf + (size_t)pid * PF_STRIDE;
+  const int on = delta ? PF_DN : PF_N, om = delta ? PF_DM : PF_M, os = delta ? PF_DS : PF_S;
+  const hipMemcpyKind k = set ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
+  HIPCHK(hipMemcpyAsync(set ? (void*)(P + on) : (void*)n, set ? (const void*)n : (const void*)(P + on), 8, k, c->stream));
+  HIPCHK(hipMemcpyAsync(set ? (void*)(P + om) : (void*)M, set ? (const void*)M : (const void*)(P + om), 8 * d, k, c->stream));
+  HIPCHK(hipMemcpyAsync(set ? (void*)(P + os) : (void*)S, set ? (const void*)S : (const void*)(P + os), 8 * d, k, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  if (set) {   // normalization constants of the restored statistics
+    launch_policy_filter(c->stream, c->route, nullptr, c->f_normc, 0.f, c->zs, c->pf, 0);
+    HIPCHK(hipStreamSynchronize(c->stream));
+  }
+  return 0;
+}
+
+int ddrl_policy_filter_set(ddrl_ctx* c, int pid, double n, const double* M, const double* S) {
+  return pf_io(c, pid, &n, const_cast<double*>(M), const_cast<double*>(S), true, false);
+}
+int ddrl_policy_filter_get(ddrl_ctx* c, int pid, double* n, double* M, double* S) {
+  return pf_io(c, pid, n, M, S, false, false);
+}
+int ddrl_policy_filter_delta_get(ddrl_ctx* c, int pid, double* n, double* M, double* S) {
+  return pf_io(c, pid, n, M, S, false, true);
+}
+int ddrl_policy_filter_delta_reset(ddrl_ctx* c) {
+  CHK_CTX(c);
+  for (int p = 0; p < c->cfg.n_policies; ++p) {
+    double* P = c->pf + (size_t)p * PF_STRIDE;
+    HIPCHK(hipMemsetAsync(P + PF_DN, 0, 8 * (1 + 2 * DDRL_MAXD), c->stream));
+  }
+  return 0;
+}
+
 int ddrl_adv_sums_get(ddrl_ctx* c, int pid, double* host3) {
   CHK_CTX(c);
   if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
@@ -360,9 +404,10 @@ int ddrl_observe(ddrl_ctx* c, const float* obs) {
   const ddrl_cfg& g = c->cfg;
   launch_filter_push(c->stream, obs, g.n_envs, g.obs_full_dim, c->f_n, c->f_M, c->f_S, c->f_normc,
                      g.filter_update, g.filter_enabled, c->f_dn, c->f_dM, c->f_dS);
+  const float clip = g.filter_enabled ? g.filter_clip : 0.f;
+  if (g.policy_filter) launch_policy_filter(c->stream, c->route, obs, c->f_normc, clip, c->zs, c->pf, 1);
   if (g.model_kind == DDRL_MODEL_FFN)
-    launch_observe_ffn(c->stream, c->route, obs, c->f_normc, g.filter_enabled ? g.filter_clip : 0.f,
-                       c->stage_tab);
+    launch_observe_ffn(c->stream, c->route, obs, c->f_normc, clip, c->stage_tab, g.policy_filter ? c->pf : nullptr);
   else
     launch_observe_gnn(c->stream, c->route, obs, c->f_normc, g.filter_enabled ? g.filter_clip : 0.f,
                        c->pol[0].stage);

@@ -39,8 +39,21 @@ struct RouteArgs {
 void launch_filter_push(hipStream_t s, const float* obs, int N, int D, double* n_run, double* M,
                         double* S, double* normc, int update, int enabled, double* dn, double* dM,
                         double* dS);
+// pf: per-policy RLlib MeanStdFilter state (PF_* layout, nullptr when disabled)
 void launch_observe_ffn(hipStream_t s, const RouteArgs& ra, const float* obs, const double* normc,
-                        float clip, float* const* stage);
+                        float clip, float* const* stage, const double* pf);
+// per-policy filter: statistics of the env-normalized observation columns, then the
+// RunningStat update + normalization constants of every policy column
+#define PF_N 0
+#define PF_M 1
+#define PF_S (PF_M + DDRL_MAXD)
+#define PF_DN (PF_S + DDRL_MAXD)
+#define PF_DM (PF_DN + 1)
+#define PF_DS (PF_DM + DDRL_MAXD)
+#define PF_NORMC (PF_DS + DDRL_MAXD)
+#define PF_STRIDE (PF_NORMC + 2 * DDRL_MAXD)
+void launch_policy_filter(hipStream_t s, const RouteArgs& ra, const float* obs, const double* normc, float clip,
+                          double* zs, double* pf, int update);
 void launch_observe_gnn(hipStream_t s, const RouteArgs& ra, const float* obs, const double* normc,
                         float clip, float* stage_x /*[N][4][23]*/);
 

@@ -81,6 +81,11 @@ void launch_filter_push(hipStream_t s, const float* obs, int N, int D, double* n
   if (enabled && update) hipLaunchKernelGGL(k_filter_count, dim3(1), dim3(1), 0, s, n_run, dn, N);
 }
 
+__device__ __forceinline__ double norm_obs_d(float x, const double* normc, int idx, float clip) {
+  double z = ((double)x - normc[2 * idx]) / normc[2 * idx + 1];
+  if (clip > 0.f) z = fmin(fmax(z, -(double)clip), (double)clip);
+  return z;
+}
 __device__ __forceinline__ float norm_obs(float x, const double* normc, int idx, float clip) {
   double z = ((double)x - normc[2 * idx]) / normc[2 * idx + 1];
   if (clip > 0.f) z = fmin(fmax(z, -(double)clip), (double)clip);
@@ -89,7 +94,8 @@ __device__ __forceinline__ float norm_obs(float x, const double* normc, int idx,
 
 // a1: per-agent gather of the normalized observation into stage[p][c][f].
 __global__ void k_observe_ffn(RouteArgs ra, const float* __restrict__ obs,
-                              const double* __restrict__ normc, float clip, float* const* stage_tab) {
+                              const double* __restrict__ normc, float clip, float* const* stage_tab,
+                              const double* __restrict__ pf) {
   const int p = blockIdx.y;
   const PolicyRoute& pr = ra.pol[p];
   const int C = ra.N * pr.k;
@@ -98,16 +104,101 @@ __global__ void k_observe_ffn(RouteArgs ra, const float* __restrict__ obs,
   const int c = gid / pr.d, f = gid - c * pr.d;
   const int e = c / pr.k, slot = c - e * pr.k;
   const int idx = pr.obs_index[slot][f];
-  stage_tab[p][(size_t)c * pr.d + f] =
-      idx >= 0 ? norm_obs(obs[(size_t)e * ra.full_dim + idx], normc, idx, clip) : (idx == -2 ? 1.f : 0.f);
+  float v;
+  if (idx < 0) {
+    v = idx == -2 ? 1.f : 0.f;
+  } else if (pf) {   // RLlib MeanStdFilter on the fp64 env-normalized value
+    const double* P = pf + (size_t)p * PF_STRIDE + PF_NORMC;
+    v = (float)((norm_obs_d(obs[(size_t)e * ra.full_dim + idx], normc, idx, clip) - P[2 * f]) / P[2 * f + 1]);
+  } else {
+    v = norm_obs(obs[(size_t)e * ra.full_dim + idx], normc, idx, clip);
+  }
+  stage_tab[p][(size_t)c * pr.d + f] = v;
 }
 
 void launch_observe_ffn(hipStream_t s, const RouteArgs& ra, const float* obs, const double* normc,
-                        float clip, float* const* stage) {
+                        float clip, float* const* stage, const double* pf) {
   int maxw = 0;
   for (int p = 0; p < ra.P; ++p) maxw = max(maxw, ra.N * ra.pol[p].k * ra.pol[p].d);
   dim3 grid((maxw + 255) / 256, ra.P);
-  hipLaunchKernelGGL(k_observe_ffn, grid, dim3(256), 0, s, ra, obs, normc, clip, stage);
+  hipLaunchKernelGGL(k_observe_ffn, grid, dim3(256), 0, s, ra, obs, normc, clip, stage, pf);
+}
+
+// ------------------------------------------------------------------------------------
+// a2 (RLlib side): per-policy MeanStdFilter, unclipped (RLlib get_filter, clip=None).
+// Policy p's rows at a step are its k agents' routed columns of every env, so the batch
+// statistics of policy column f are sums of the env-normalized full-observation column
+// statistics over the slots: one fp64 pass over obs [N][D] (k_zstats) serves every policy.
+// The batch is merged with RunningStat.update (Chan), like the env-side filter.
+// ------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_zstats(const float* __restrict__ obs, int N, int D,
+                                                const double* __restrict__ normc, float clip,
+                                                double* __restrict__ zs) {
+  const int j = blockIdx.x, tid = threadIdx.x;
+  __shared__ double red[2][4];
+  double s1 = 0.0, s2 = 0.0;
+  for (int e = tid; e < N; e += 256) {
+    const double z = norm_obs_d(obs[(size_t)e * D + j], normc, j, clip);
+    s1 += z;
+    s2 += z * z;
+  }
+  s1 = wave_sum_d(s1);
+  s2 = wave_sum_d(s2);
+  if ((tid & 63) == 0) { red[0][tid >> 6] = s1; red[1][tid >> 6] = s2; }
+  __syncthreads();
+  if (tid == 0) {
+    zs[2 * j] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    zs[2 * j + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+  }
+}
+
+__device__ __forceinline__ void chan_merge(double& n, double& M, double& S, double nb, double mb, double sb) {
+  const double tot = n + nb, delta = M - mb;
+  M = (n * M + nb * mb) / tot;
+  S = S + sb + delta * delta * n * nb / tot;
+}
+
+__global__ void k_pfilter(RouteArgs ra, const double* __restrict__ zs, double* pf, int update) {
+  const int p = blockIdx.x, f = threadIdx.x;
+  const PolicyRoute& pr = ra.pol[p];
+  double* P = pf + (size_t)p * PF_STRIDE;
+  const double n0 = P[PF_N], dn0 = P[PF_DN];
+  const double nb = (double)ra.N * pr.k;
+  __syncthreads();
+  if (f < pr.d) {
+    double M = P[PF_M + f], S = P[PF_S + f], n = n0;
+    if (update) {
+      double s1 = 0.0, s2 = 0.0;
+      for (int s = 0; s < pr.k; ++s) {
+        const int idx = pr.obs_index[s][f];
+        s1 += zs[2 * idx];
+        s2 += zs[2 * idx + 1];
+      }
+      const double mb = s1 / nb, sb = fmax(s2 - s1 * mb, 0.0);
+      chan_merge(n, M, S, nb, mb, sb);
+      double dn = dn0, dM = P[PF_DM + f], dS = P[PF_DS + f];
+      chan_merge(dn, dM, dS, nb, mb, sb);
+      P[PF_M + f] = M;
+      P[PF_S + f] = S;
+      P[PF_DM + f] = dM;
+      P[PF_DS + f] = dS;
+      n = n0 + nb;
+    }
+    const double var = n > 1.0 ? S / (n - 1.0) : M * M;
+    P[PF_NORMC + 2 * f] = M;
+    P[PF_NORMC + 2 * f + 1] = sqrt(var) + 1e-8;
+  }
+  __syncthreads();
+  if (update && f == 0) {
+    P[PF_N] = n0 + nb;
+    P[PF_DN] = dn0 + nb;
+  }
+}
+
+void launch_policy_filter(hipStream_t s, const RouteArgs& ra, const float* obs, const double* normc, float clip,
+                          double* zs, double* pf, int update) {
+  if (update) hipLaunchKernelGGL(k_zstats, dim3(ra.full_dim), dim3(256), 0, s, obs, ra.N, ra.full_dim, normc, clip, zs);
+  hipLaunchKernelGGL(k_pfilter, dim3(ra.P), dim3(64), 0, s, ra, zs, pf, update);
 }
 
 // a3: graph observation X[env][node] = [normalized 19 features | ego quaternion (raw obs)].

@@ -38,7 +38,7 @@ class DdrlCfg(C.Structure):
         ("vf_loss_coeff", f32), ("entropy_coeff", f32), ("lr", f32), ("grad_clip", f32),
         ("adam_beta1", f32), ("adam_beta2", f32), ("adam_eps", f32),
         ("vf_clip_mode", i32), ("sgd_minibatch_size", i32), ("num_sgd_iter", i32),
-        ("act_negate", (i32 * 8) * MAX_AG),
+        ("act_negate", (i32 * 8) * MAX_AG), ("policy_filter", i32),
     ]
 
 
@@ -61,6 +61,10 @@ _SIGS = {
     "ddrl_filter_delta_get": ([VP, C.POINTER(C.c_double), VP, VP], C.c_int),
     "ddrl_filter_delta_reset": ([VP], C.c_int),
     "ddrl_adv_sums_get": ([VP, C.c_int, VP], C.c_int),
+    "ddrl_policy_filter_set": ([VP, C.c_int, C.c_double, VP, VP], C.c_int),
+    "ddrl_policy_filter_get": ([VP, C.c_int, C.POINTER(C.c_double), VP, VP], C.c_int),
+    "ddrl_policy_filter_delta_get": ([VP, C.c_int, C.POINTER(C.c_double), VP, VP], C.c_int),
+    "ddrl_policy_filter_delta_reset": ([VP], C.c_int),
     "ddrl_observe": ([VP, VP], C.c_int),
     "ddrl_act": ([VP, C.c_int, VP, VP], C.c_int),
     "ddrl_reward": ([VP, C.c_int, VP, VP, VP, VP], C.c_int),
@@ -217,6 +221,22 @@ class Context:
 
     def filter_delta_reset(self):
         _ck(self.lib.ddrl_filter_delta_reset(self.h))
+
+    def policy_filter_set(self, pid, n, M, S):
+        M = np.ascontiguousarray(M, np.float64)
+        S = np.ascontiguousarray(S, np.float64)
+        _ck(self.lib.ddrl_policy_filter_set(self.h, pid, float(n), M.ctypes.data, S.ctypes.data))
+
+    def policy_filter_get(self, pid, delta=False):
+        d = self.cfg.obs_dim[pid]
+        n = C.c_double()
+        M, S = np.empty(d), np.empty(d)
+        fn = self.lib.ddrl_policy_filter_delta_get if delta else self.lib.ddrl_policy_filter_get
+        _ck(fn(self.h, pid, C.byref(n), M.ctypes.data, S.ctypes.data))
+        return n.value, M, S
+
+    def policy_filter_delta_reset(self):
+        _ck(self.lib.ddrl_policy_filter_delta_reset(self.h))
 
     def adv_sums_get(self, pid):
         """fp64 (sum adv, sum adv^2, count) of the last gae() for policy pid."""

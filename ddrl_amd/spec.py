@@ -17,6 +17,9 @@ PPO_DEFAULTS = {
     "lr": 3e-4, "grad_clip": 0.5, "sgd_minibatch_size": 128, "num_sgd_iter": 10,
     "train_batch_size": 16000, "rollout_fragment_length": 200, "shuffle_sequences": True,
     "clip_actions": True, "vf_clip_mode": "ray10",
+    # RLlib-side per-policy filter: exp-1 in the fork uses NoFilter (train_experiment_1:128);
+    # the published runs and the shared-policy script use MeanStdFilter (P_Local:139)
+    "observation_filter": "NoFilter",
 }
 ENV_DEFAULTS = {"ctrl_cost_weight": 0.5, "contact_cost_weight": 5e-2, "hf_smoothness": 1.0,
                 "norm_reward": False, "global_reward": False, "filter_clip": 10.0,
@@ -81,4 +84,7 @@ def make_cfg(env, n_envs, frag_len=None, config=None):
     c.vf_clip_mode = N.VF_CLIP_RAY10 if config["vf_clip_mode"] == "ray10" else N.VF_CLIP_SQUARED
     c.sgd_minibatch_size = int(config["sgd_minibatch_size"])
     c.num_sgd_iter = int(config["num_sgd_iter"])
+    if config["observation_filter"] not in ("NoFilter", "MeanStdFilter"):
+        raise ValueError(f"observation_filter {config['observation_filter']!r} is not supported")
+    c.policy_filter = 1 if config["observation_filter"] == "MeanStdFilter" else 0
     return c, inst

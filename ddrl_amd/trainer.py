@@ -91,6 +91,9 @@ class PPOTrainer:
                                                c.get("ddp_mode", "split"))
             self.filter_base = self.ctx.filter_get()
             self.ctx.filter_delta_reset()
+            self.pfilter_base = ([self.ctx.policy_filter_get(p) for p in range(P)]
+                                 if self.cfg.policy_filter else None)
+            self.ctx.policy_filter_delta_reset()
             self.grad = torch.zeros(self.ctx.n_params[0], dtype=torch.float32, device=self.device)
         self.ctx.observe(self.backend.reset())
 
@@ -112,6 +115,12 @@ class PPOTrainer:
             self.ctx.filter_set(*merged)
             self.ctx.filter_delta_reset()
             self.filter_base = merged
+            if self.pfilter_base is not None:   # RLlib synchronize_filters for the policy filters
+                for p in range(self.cfg.n_policies):
+                    self.pfilter_base[p] = sync_filters(self.comm, self.pfilter_base[p],
+                                                        self.ctx.policy_filter_get(p, delta=True))
+                    self.ctx.policy_filter_set(p, *self.pfilter_base[p])
+                self.ctx.policy_filter_delta_reset()
             for p in range(self.cfg.n_policies):
                 self.ctx.adv_norm_set(p, *sync_standardize(self.comm, self.ctx.adv_sums_get(p)))
 
@@ -208,6 +217,10 @@ class PPOTrainer:
             arrs[f"{pid}/kl_coeff"] = np.array([self.kl_coeff[p]])
         n, M, S = self.ctx.filter_get()
         arrs["filter/n"], arrs["filter/M"], arrs["filter/S"] = np.array([n]), M, S
+        if self.cfg.policy_filter:
+            for p, pid in enumerate(self.policy_ids):
+                n, M, S = self.ctx.policy_filter_get(p)
+                arrs[f"{pid}/filter/n"], arrs[f"{pid}/filter/M"], arrs[f"{pid}/filter/S"] = np.array([n]), M, S
         arrs["meta"] = np.frombuffer(json.dumps({"iteration": self.iteration,
                                                  "timesteps_total": self.timesteps_total}).encode(), np.uint8)
         np.savez(path, **arrs)
@@ -221,6 +234,10 @@ class PPOTrainer:
             self.ctx.adam_set(p, z[f"{pid}/adam_m"], z[f"{pid}/adam_v"], float(b[0]), float(b[1]))
             self.kl_coeff[p] = float(z[f"{pid}/kl_coeff"][0])
         self.ctx.filter_set(float(z["filter/n"][0]), z["filter/M"], z["filter/S"])
+        if self.cfg.policy_filter:
+            for p, pid in enumerate(self.policy_ids):
+                self.ctx.policy_filter_set(p, float(z[f"{pid}/filter/n"][0]), z[f"{pid}/filter/M"],
+                                           z[f"{pid}/filter/S"])
         meta = json.loads(bytes(z["meta"]).decode())
         self.iteration, self.timesteps_total = meta["iteration"], meta["timesteps_total"]
 

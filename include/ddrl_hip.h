@@ -73,6 +73,8 @@ typedef struct ddrl_cfg {
   int32_t num_sgd_iter;        /* 10                                                       */
   int32_t act_negate[DDRL_MAX_AGENTS][8];  /* 1: negate action j of the agent in the env action
                                               vector (LegTransforms: fr / hr knee)          */
+  int32_t policy_filter;    /* RLlib observation_filter "MeanStdFilter" on every policy's
+                               input (after the env-side filter; unclipped, fp64 stats)     */
 } ddrl_cfg;
 
 typedef struct ddrl_ctx ddrl_ctx;
@@ -107,6 +109,12 @@ int ddrl_filter_get(ddrl_ctx* ctx, double* n, double* mean_host, double* sq_host
  * (RunningStat.update in rank order) and resets (synchronize_filters, P_Local:160). */
 int ddrl_filter_delta_get(ddrl_ctx* ctx, double* n, double* mean_host, double* sq_host);
 int ddrl_filter_delta_reset(ddrl_ctx* ctx);
+/* The per-policy RLlib MeanStdFilter (cfg.policy_filter): RunningStat of policy pid over its
+ * obs_dim input columns, and its pushes since the last delta reset (same sync protocol). */
+int ddrl_policy_filter_set(ddrl_ctx* ctx, int pid, double n, const double* mean_host, const double* sq_host);
+int ddrl_policy_filter_get(ddrl_ctx* ctx, int pid, double* n, double* mean_host, double* sq_host);
+int ddrl_policy_filter_delta_get(ddrl_ctx* ctx, int pid, double* n, double* mean_host, double* sq_host);
+int ddrl_policy_filter_delta_reset(ddrl_ctx* ctx);
 
 /* Rollout (per env step).
  * observe: env-side MeanStdFilter push + normalize + per-agent routing of the raw

@@ -62,6 +62,9 @@ class OracleRollout:
                                  rew=np.zeros((T, C), np.float32)))
         self.done = np.zeros((T, N_), np.uint8)
         self.stage = None
+        # RLlib per-policy MeanStdFilter (observation_filter), unclipped, on the fp64 routed rows
+        self.pf = ([O.RunningStat((cfg.obs_dim[p],)) for p in range(cfg.n_policies)]
+                   if getattr(cfg, "policy_filter", 0) else None)
 
     def observe(self, obs):
         normed = O.mean_std_filter(obs, self.rs, update=True, clip=self.cfg.filter_clip)
@@ -73,6 +76,8 @@ class OracleRollout:
         for p in range(self.cfg.n_policies):
             cols = [ext[:, [col(i) for i in tables[a]]] for a in self.slots[p]]
             x = np.stack(cols, 1).reshape(-1, self.cfg.obs_dim[p])   # c = e * k + slot
+            if self.pf is not None:
+                x = O.mean_std_filter(x, self.pf[p], update=True, clip=None)
             self.stage.append(x.astype(np.float32))
 
     def act(self, t, eps):

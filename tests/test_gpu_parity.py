@@ -76,6 +76,38 @@ def test_rollout_gae_parity(env, n, T):
     ctx.close()
 
 
+@pytest.mark.parametrize("env,n,T", [("QuantrupedMultiEnv_Local", 40, 5),
+                                     ("QuantrupedMultiEnv_SharedDecentral", 24, 4)])
+def test_rollout_with_policy_mean_std_filter(env, n, T):
+    """observation_filter = MeanStdFilter: RLlib's per-policy RunningStat (unclipped) on top of
+    the env-side filter; batched Chan merges on the device vs per-row pushes in the oracle."""
+    ctx, cfg, inst = make_ctx(env, n, T, {"observation_filter": "MeanStdFilter"})
+    assert cfg.policy_filter == 1
+    rng = np.random.default_rng(17)
+    params = init_params(ctx, cfg, 4)
+    orc, norms, a_gpu, a_orc = run_rollout(ctx, cfg, inst, params, rng, _filt(cfg.obs_full_dim, rng), T)
+    _close(a_gpu, a_orc, msg="env actions")
+    for p in range(cfg.n_policies):
+        pn, pM, pS = ctx.policy_filter_get(p)
+        assert pn == orc.pf[p].n
+        _close(pM, orc.pf[p].M, rtol=1e-10, atol=1e-10)
+        _close(pS, orc.pf[p].S, rtol=1e-9, atol=1e-8)
+        dn, dM, dS = ctx.policy_filter_get(p, delta=True)
+        assert dn == pn   # no sync yet: the delta is everything pushed
+        lay = ctx.layout[p]
+        got, ref = ctx.records_get(p), orc.flat_records(p, lay)
+        d, A = cfg.obs_dim[p], cfg.act_dim
+        _close(got[:, :d], ref[:, :d], rtol=1e-5, atol=2e-5, msg="filtered obs")
+        _close(got[:, lay["logit"]:lay["logit"] + 2 * A], ref[:, lay["logit"]:lay["logit"] + 2 * A],
+               rtol=1e-5, atol=2e-5, msg="logits")
+    # set / get round trip recomputes the normalization constants
+    pn, pM, pS = ctx.policy_filter_get(0)
+    ctx.policy_filter_set(0, pn, pM * 0.5, pS)
+    n2, M2, _ = ctx.policy_filter_get(0)
+    assert n2 == pn and np.array_equal(M2, pM * 0.5)
+    ctx.close()
+
+
 def _batch_from_records(rec, lay, d, A, adv_norm):
     mean, den = adv_norm
     return dict(obs=rec[:, lay["obs"]:lay["obs"] + d], actions=rec[:, lay["act"]:lay["act"] + A],

@@ -64,7 +64,7 @@ def test_trainer_ddp_world1(pg1, tmp_path):
     grad / all-reduce / apply) on one rank; save / restore round trip."""
     from ddrl_amd.trainer import PPOTrainer
     tr = PPOTrainer({"env": "QuantrupedMultiEnv_SharedDecentral", "rollout_fragment_length": 8,
-                     "parallel": "ddp"}, n_envs=32, seed=1)
+                     "parallel": "ddp", "observation_filter": "MeanStdFilter"}, n_envs=32, seed=1)
     assert tr.parallel == "ddp"
     r = tr.train()
     st = r["info"]["learner"]["policy_legs"] if "policy_legs" in r["info"]["learner"] else \
@@ -72,6 +72,8 @@ def test_trainer_ddp_world1(pg1, tmp_path):
     assert np.isfinite(st["kl"]) and st["num_ranks"] == 1
     n, M, S = tr.ctx.filter_get()
     assert n == 32 * 9   # reset + 8 steps pushed, synced into the base filter
+    pn, _, _ = tr.ctx.policy_filter_get(0)
+    assert pn == 32 * 4 * 9 and tr.ctx.policy_filter_get(0, delta=True)[0] == 0   # synced, delta reset
     path = tr.save(str(tmp_path / "ck.npz"))
     w = tr.get_weights()
     tr.train()
