@@ -425,9 +425,15 @@ __global__ void __launch_bounds__(256) k_gnn(GnnArgs ga) {
 __global__ void __launch_bounds__(256) k_gnn_reduce(GnnArgs ga, int ntiles, int n) {
   __shared__ float red[4];
   const int p = blockIdx.x * 256 + threadIdx.x;
+  // all tile partials of this parameter in flight at once (a runtime-bound loop would wait
+  // for each load before the next add), then summed in tile order
+  float v[DDRL_MB / 4];
+#pragma unroll
+  for (int t = 0; t < DDRL_MB / 4; ++t)
+    v[t] = (p < n && t < ntiles) ? ga.part[(size_t)t * ga.part_stride + p] : 0.f;
   float s = 0.f;
-  if (p < n)
-    for (int t = 0; t < ntiles; ++t) s += ga.part[(size_t)t * ga.part_stride + p];
+#pragma unroll
+  for (int t = 0; t < DDRL_MB / 4; ++t) s += v[t];
   if (p < n) ga.grad[p] = s;
   float ss = wave_sum(s * s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
@@ -438,8 +444,12 @@ __global__ void __launch_bounds__(256) k_gnn_reduce(GnnArgs ga, int ntiles, int 
     // j over the tiles (independent loads), lane 64 combines
     __shared__ float sv[10];
     const int j = threadIdx.x - 64, b = j / 5, k = j - 5 * b;
+    float sv_t[DDRL_MB / 4];
+#pragma unroll
+    for (int t = 0; t < DDRL_MB / 4; ++t) sv_t[t] = t < ntiles ? ga.statp[(b * DDRL_MB / 4 + t) * 8 + k] : 0.f;
     float a = 0.f;
-    for (int t = 0; t < ntiles; ++t) a += ga.statp[(b * DDRL_MB / 4 + t) * 8 + k];
+#pragma unroll
+    for (int t = 0; t < DDRL_MB / 4; ++t) a += sv_t[t];
     sv[j] = a;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
