@@ -201,9 +201,9 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
        dalloc(c, &c->h_eps, (size_t)N * g.n_agents * g.act_dim) || dalloc(c, &c->h_act, (size_t)N * 8);
   if (!rc && g.model_kind == DDRL_MODEL_GNN) {
     const int np = c->pol[0].n_params;
-    c->gnn.part_stride = np;
+    c->gnn.part_stride = (np + 3) & ~3;   // 16-byte aligned tile rows (float4 partial stores)
     c->gnn.grad = c->pol[0].grad;
-    rc = dalloc(c, &c->gnn.part, (size_t)(DDRL_MB / 4) * np) || dalloc(c, &c->gnn.statp, 2 * (DDRL_MB / 4) * 8) ||
+    rc = dalloc(c, &c->gnn.part, (size_t)(DDRL_MB / 4) * c->gnn.part_stride) || dalloc(c, &c->gnn.statp, 2 * (DDRL_MB / 4) * 8) ||
          dalloc(c, &c->gnn.normp, (np + 255) / 256) || dalloc(c, &c->gnn.bp_cur, 2);
   }
   if (!rc) {

@@ -66,7 +66,9 @@ __device__ __forceinline__ float quad_next(float v) { return dpp_mov<0x39>(v); }
 #define L_DOUT (L_HP + 256)
 #define L_ST (L_DOUT + 16)
 #define L_SEL (L_ST + 32)
-#define L_TOTAL (L_SEL + 8)
+#define L_TP (L_SEL + 8)          // per-wave 4 x 16x16 transpose tiles of the hypernet backward
+#define L_QT (L_TP + 4 * 1024)    // quaternions of the tile's 16 graph-nodes [16][4]
+#define L_TOTAL (L_QT + 64)
 
 template <int A, int MODE, int NET>
 __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
@@ -79,6 +81,9 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
   const GnnNetOff off = gnn_net_off(A, NET);
   const float* __restrict__ th = ga.theta;
   if (MODE == GNN_ACT && NET == 0 && ga.bootstrap) return;   // bootstrap: critic only
+#ifdef DDRL_ABL_GNN_EMPTY
+  if (MODE == GNN_GRAD) return;
+#endif
 
   // ---- locate this lane's graph (X [4][23]) and the selected node ----
   const float* X;
@@ -138,6 +143,9 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
   for (int t = 0; t < 4; ++t) hacc[t] = splat4(0.f);
 #pragma unroll
   for (int k = 0; k < GNI; ++k) {
+#ifdef DDRL_ABL_GNN_NO_HFWD
+    break;
+#endif
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const floatx4 pre = mfma4(we[k][t], qv, be[k][t]);
@@ -380,11 +388,23 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
   for (int t = 0; t < 4; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) dz[t][r] = part[(4 * t + r) * 64 + lane];
-  float qa[4];
+#ifdef DDRL_ABL_GNN_NO_HBWD   // ablation build (timing only)
+  return;
+#endif
+  // hypernet backward: recompute W_n column blocks, dpre = f_i dz (1 - W^2); then
+  //   [dWenc | dbenc] (block j, qd) = sum over the 16 rows of dpre[row][j] [q_row | 1][qd]
+  // as 4 MFMAs per block: dpre goes through a per-wave LDS tile to put rows on the k axis,
+  // B = the rows' quaternions with a ones column (bias) at qd = 4.
+  float* qt = lds + L_QT;
+  if (w == 0 && q == 0) {
 #pragma unroll
-  for (int d = 0; d < 4; ++d) qa[d] = xr[GF + d];
-  // hypernet backward: recompute W_n rows, dpre = f_i dz (1 - W^2); dWenc = q^T dpre,
-  // dbenc = sum of dpre, both reduced over the 16 rows of the DPP row.
+    for (int d = 0; d < 4; ++d) qt[c * 4 + d] = xr[GF + d];
+  }
+  __syncthreads();
+  float qb[4];
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) qb[s4] = c < 4 ? qt[(4 * s4 + q) * 4 + c] : (c == 4 ? 1.f : 0.f);
+  float* tp = lds + L_TP + 1024 * w;   // one 16x16 tile per column block t
 #pragma unroll
   for (int k = 0; k < GNI; ++k) {
     const int i = w + 4 * k;
@@ -392,24 +412,26 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const floatx4 pre = mfma4(we[k][t], qv, be[k][t]);
-      float dp[4];
+      floatx4 dp;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const float wn = tanh_fast(pre[r]);
         dp[r] = fi[k] * dz[t][r] * (1.f - wn * wn);
       }
-      float v[16];
+      *reinterpret_cast<floatx4*>(tp + 256 * t + c * 16 + 4 * q) = dp;   // [row c][j 4q + r]
+    }
+    floatx4 acc[4];
 #pragma unroll
-      for (int d = 0; d < 4; ++d)
+    for (int t = 0; t < 4; ++t) acc[t] = splat4(0.f);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[4 * d + r] = qa[d] * dp[r];
-      const float s = row16_transpose_sum(v);
-      const int j = i * 64 + 16 * t + 4 * q;
-      P[off.wenc + (c >> 2) * GHE + j + (c & 3)] = s;
-      float b[4];
+    for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) b[r] = row16_sum(dp[r]);
-      if (c < 4) P[off.benc + j + c] = c == 0 ? b[0] : c == 1 ? b[1] : c == 2 ? b[2] : b[3];
+      for (int t = 0; t < 4; ++t) acc[t] = mfma4(tp[256 * t + (4 * s4 + q) * 16 + c], qb[s4], acc[t]);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int j = i * 64 + 16 * t + 4 * q;                  // acc[r]: column j + r, qd = c
+      if (c < 4) *reinterpret_cast<floatx4*>(P + off.wenc + c * GHE + j) = acc[t];
+      else if (c == 4) *reinterpret_cast<floatx4*>(P + off.benc + j) = acc[t];
     }
   }
 }
