@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -59,6 +60,8 @@ struct ddrl_ctx {
   int32_t* zero_perm = nullptr;
   UpdateArgs* d_uargs = nullptr;  // device copy of the per-workgroup update arguments
   unsigned long long* xchg = nullptr;  // norm^2 exchange granules of the update kernel
+  unsigned long long* gx = nullptr;    // partial-gradient granules of the row-split update
+  int update_split = 2;                // workgroups per branch of the fused update (1 or 2)
   int* err = nullptr;                  // device error word (exchange timeout)
   float kl_last[DDRL_MAXP] = {0};
   GnnScratch gnn{};               // GraphNet step scratch (per-tile partial gradients, ...)
@@ -146,6 +149,8 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
   if (device < 0 || device >= ndev) return fail("device index out of range");
   HIPCHK(hipSetDevice(device));
   ddrl_ctx* c = new ddrl_ctx();
+  // fused update geometry: DDRL_UPDATE_SPLIT=1 keeps one workgroup per branch (timing / A-B)
+  if (const char* e = std::getenv("DDRL_UPDATE_SPLIT")) c->update_split = std::atoi(e) == 1 ? 1 : 2;
   c->cfg = *cfg;
   c->device = device;
   const ddrl_cfg& g = c->cfg;
@@ -196,7 +201,8 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
        dalloc(c, &c->f_dM, DDRL_MAXFULL) || dalloc(c, &c->f_dS, DDRL_MAXFULL) ||
        dalloc(c, &c->pf, (size_t)DDRL_MAXP * PF_STRIDE) || dalloc(c, &c->zs, 2 * DDRL_MAXFULL) || dalloc(c, &c->done_tn, (size_t)T * N) ||
        dalloc(c, &c->stage_tab, DDRL_MAXP) || dalloc(c, &c->zero_perm, 4) ||
-       dalloc(c, &c->d_uargs, DDRL_MAXP) || dalloc(c, &c->xchg, 4 * DDRL_MAXP) || dalloc(c, &c->err, 1) ||
+       dalloc(c, &c->d_uargs, DDRL_MAXP) || dalloc(c, &c->xchg, 8 * DDRL_MAXP) ||
+       dalloc(c, &c->gx, gx_bytes(DDRL_MAXP) / sizeof(unsigned long long)) || dalloc(c, &c->err, 1) ||
        dalloc(c, &c->h_obs, (size_t)N * g.obs_full_dim) ||
        dalloc(c, &c->h_eps, (size_t)N * g.n_agents * g.act_dim) || dalloc(c, &c->h_act, (size_t)N * 8);
   if (!rc && g.model_kind == DDRL_MODEL_GNN) {
@@ -546,7 +552,7 @@ int ddrl_ppo_update(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const 
   HIPCHK(hipMemcpyAsync(c->d_uargs, ua, sizeof(UpdateArgs) * n, hipMemcpyHostToDevice, c->stream));
   if (c->cfg.model_kind == DDRL_MODEL_FFN)
     launch_update_ffn(c->stream, c->d_uargs, h, 128, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim, maxd,
-                      c->xchg, c->err);
+                      c->xchg, c->gx, c->update_split, c->err);
   else
     for (int step = 0; step < c->pol[0].last_steps; ++step)   // one shared policy
       launch_step_gnn(c->stream, ua[0], h, step, 128, 1.f / c->cfg.sgd_minibatch_size, c->gnn);
@@ -588,7 +594,7 @@ int ddrl_ppo_grad(ddrl_ctx* c, int pid, const int32_t* rows, int n_rows, float k
   HIPCHK(hipMemcpyAsync(c->d_uargs, &u, sizeof(UpdateArgs), hipMemcpyHostToDevice, c->stream));
   if (c->cfg.model_kind == DDRL_MODEL_FFN)
     launch_update_ffn(c->stream, c->d_uargs, h, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim,
-                      c->pol[pid].d, c->xchg, c->err);
+                      c->pol[pid].d, c->xchg, c->gx, 1, c->err);
   else
     launch_step_gnn(c->stream, u, h, 0, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->gnn);
   HIPCHK(hipGetLastError());

@@ -23,6 +23,7 @@
 #include <stdint.h>
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 #define DDRL_H 64          // hidden width (fcnet_hiddens = [64, 64])
 #ifndef DDRL_MB
@@ -189,19 +190,43 @@ __device__ __forceinline__ void ffn_fwd_rt(const NetLds& W, const float (*xop)[1
 #pragma unroll
     for (int t = 0; t < RT; ++t) h1[t][ob] = b;
   }
+  // Weight operands of k-step s + 2 are loaded while the MFMAs of step s issue (a 3-deep
+  // register ring; the scheduling barrier keeps the compiler from sinking the loads next to
+  // their MFMAs, which a single wave per SIMD cannot hide).
+  const int rb[4] = {rbase(0), rbase(1), rbase(2), rbase(3)};
+  auto ld1 = [&](int s, float* a) {
+    const float* wp = W.w1 + rb[s & 3] + 1024 * (s >> 2);
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) a[ob] = wp[16 * ob];
+  };
+  int fb_base[4];   // layer 2: row f = 16fb + 4q + r -> same swizzle as rbase with (4q + r) as the row
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = 4 * q + r;
+    fb_base[r] = row * 64 + (c ^ swz(row));
+  }
+  auto ld2 = [&](int k, float* a) {   // k = 4 fb + r
+    const float* wp = W.w2 + fb_base[k & 3] + 1024 * (k >> 2);
+#pragma unroll
+    for (int ob = 0; ob < 4; ++ob) a[ob] = wp[16 * ob];
+  };
+  float wr[3][4];
   {
-    const int rb[4] = {rbase(0), rbase(1), rbase(2), rbase(3)};
+    ld1(0, wr[0]);
+    if (KS1 > 1) ld1(1, wr[1]);
 #pragma unroll
     for (int s = 0; s < KS1; ++s) {
-      const float* wp = W.w1 + rb[s & 3] + 1024 * (s >> 2);
+      if (s + 2 < KS1) ld1(s + 2, wr[(s + 2) % 3]);
 #pragma unroll
-      for (int ob = 0; ob < 4; ++ob) {
-        const float a = wp[16 * ob];
+      for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
-        for (int t = 0; t < RT; ++t) h1[t][ob] = mfma4(a, xop[t][s], h1[t][ob]);
-      }
+        for (int t = 0; t < RT; ++t) h1[t][ob] = mfma4(wr[s % 3][ob], xop[t][s], h1[t][ob]);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
+  float wq[3][4];
+  ld2(0, wq[0]);
+  ld2(1, wq[1]);
 #pragma unroll
   for (int t = 0; t < RT; ++t)
 #pragma unroll
@@ -217,25 +242,15 @@ __device__ __forceinline__ void ffn_fwd_rt(const NetLds& W, const float (*xop)[1
     for (int t = 0; t < RT; ++t) h2[t][ob] = b;
   }
   {
-    // row f = 16fb + 4q + r  ->  same swizzle as rbase with (4q + r) as the row
-    int fb_base[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = 4 * q + r;
-      fb_base[r] = row * 64 + (c ^ swz(row));
+    for (int k = 0; k < 16; ++k) {
+      if (k + 2 < 16) ld2(k + 2, wq[(k + 2) % 3]);
+#pragma unroll
+      for (int ob = 0; ob < 4; ++ob)
+#pragma unroll
+        for (int t = 0; t < RT; ++t) h2[t][ob] = mfma4(wq[k % 3][ob], h1[t][k >> 2][k & 3], h2[t][ob]);
+      __builtin_amdgcn_sched_barrier(0);
     }
-#pragma unroll
-    for (int fb = 0; fb < 4; ++fb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float* wp = W.w2 + fb_base[r] + 1024 * fb;
-#pragma unroll
-        for (int ob = 0; ob < 4; ++ob) {
-          const float a = wp[16 * ob];
-#pragma unroll
-          for (int t = 0; t < RT; ++t) h2[t][ob] = mfma4(a, h1[t][fb][r], h2[t][ob]);
-        }
-      }
   }
 #pragma unroll
   for (int t = 0; t < RT; ++t)
@@ -304,18 +319,23 @@ __device__ __forceinline__ void layer2_bwd_rt(const NetLds& W, const floatx4 (*d
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) dh1[t][fb] = splat4(0.f);
   const int wb[4] = {wbase(0), wbase(1), wbase(2), wbase(3)};
-#pragma unroll 2
-  for (int ob = 0; ob < 4; ++ob)
+  auto ld = [&](int k, float* a) {   // k = 4 ob + r (operands prefetched two steps ahead)
+    const float* wp = W.w2 + wb[k & 3] + 16 * (k >> 2);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float* wp = W.w2 + wb[r] + 16 * ob;
+    for (int fb = 0; fb < 4; ++fb) a[fb] = wp[1024 * fb];
+  };
+  float wr[3][4];
+  ld(0, wr[0]);
+  ld(1, wr[1]);
 #pragma unroll
-      for (int fb = 0; fb < 4; ++fb) {
-        const float a = wp[1024 * fb];
+  for (int k = 0; k < 16; ++k) {
+    if (k + 2 < 16) ld(k + 2, wr[(k + 2) % 3]);
 #pragma unroll
-        for (int t = 0; t < RT; ++t) dh1[t][fb] = mfma4(a, dz2[t][ob][r], dh1[t][fb]);
-      }
-    }
+    for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+      for (int t = 0; t < RT; ++t) dh1[t][fb] = mfma4(wr[k % 3][fb], dz2[t][k >> 2][k & 3], dh1[t][fb]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
 }
 __device__ __forceinline__ void layer2_bwd(const NetLds& W, const floatx4 dz2[4], floatx4 dh1[4]) {
   layer2_bwd_rt<1>(W, reinterpret_cast<const floatx4 (*)[4]>(dz2), reinterpret_cast<floatx4 (*)[4]>(dh1));
@@ -337,35 +357,46 @@ __device__ __forceinline__ void store_act(float* buf, int tile, const floatx4 v[
 // of the dW operands bank-conflict free).  The GEMM's k index is the row b; lane (c, q)
 // takes rows 16u + 4q .. 16u + 4q + 3 for k-group u, i.e. ONE ds_read_b128 per operand per
 // four MFMAs.
+// (A 64-row image uses stride 72, also 8 mod 64.)
 #define FM_LD 136
+template <int LD = FM_LD>
 __device__ __forceinline__ void store_act_fm(float* buf, int tile, const floatx4 v[4]) {
   const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
-  float* p = buf + (4 * q) * FM_LD + 16 * tile + c;
+  float* p = buf + (4 * q) * LD + 16 * tile + c;
 #pragma unroll
   for (int fb = 0; fb < 4; ++fb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) p[(16 * fb + r) * FM_LD] = v[fb][r];
+    for (int r = 0; r < 4; ++r) p[(16 * fb + r) * LD] = v[fb][r];
 }
 
 // NT_ tiles dW[f = 16 fa_i + 4q + r][o = 16 fo + c] (one fo, NT_ fa's) over NROWS rows.
-template <int NROWS, int NT_>
+template <int NROWS, int NT_, int LD = NROWS + 8>
 __device__ __forceinline__ void dw_tiles_fm(const float* A, const float* B, const int* fa, int fo, floatx4* out) {
   const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
 #pragma unroll
   for (int i = 0; i < NT_; ++i) out[i] = splat4(0.f);
-  const float* bp = B + (16 * fo + c) * FM_LD + 4 * q;
+  const float* bp = B + (16 * fo + c) * LD + 4 * q;
   const float* ap[NT_];
 #pragma unroll
-  for (int i = 0; i < NT_; ++i) ap[i] = A + (16 * fa[i] + c) * FM_LD + 4 * q;
-#pragma unroll 2
-  for (int u = 0; u < NROWS / 16; ++u) {
-    const floatx4 bv = *reinterpret_cast<const floatx4*>(bp + 16 * u);
+  for (int i = 0; i < NT_; ++i) ap[i] = A + (16 * fa[i] + c) * LD + 4 * q;
+  // operands of row group u + 1 are loaded while the MFMAs of group u issue
+  constexpr int NU = NROWS / 16;
+  floatx4 bv[2], av[2][NT_];
+  bv[0] = *reinterpret_cast<const floatx4*>(bp);
 #pragma unroll
-    for (int i = 0; i < NT_; ++i) {
-      const floatx4 av = *reinterpret_cast<const floatx4*>(ap[i] + 16 * u);
+  for (int i = 0; i < NT_; ++i) av[0][i] = *reinterpret_cast<const floatx4*>(ap[i]);
 #pragma unroll
-      for (int v = 0; v < 4; ++v) out[i] = mfma4(av[v], bv[v], out[i]);
+  for (int u = 0; u < NU; ++u) {
+    if (u + 1 < NU) {
+      bv[(u + 1) & 1] = *reinterpret_cast<const floatx4*>(bp + 16 * (u + 1));
+#pragma unroll
+      for (int i = 0; i < NT_; ++i) av[(u + 1) & 1][i] = *reinterpret_cast<const floatx4*>(ap[i] + 16 * (u + 1));
     }
+#pragma unroll
+    for (int i = 0; i < NT_; ++i)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) out[i] = mfma4(av[u & 1][i][v], bv[u & 1][v], out[i]);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 

@@ -122,8 +122,10 @@ struct UpdateHyper {
   int P;
 };
 // ua_dev: device array of h.P UpdateArgs (one persistent workgroup per entry)
+// ksp: 1 = one workgroup per branch, 2 = row split over two (gx: gx_bytes(P) of exchange granules)
 void launch_update_ffn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHyper& h, int nrows, float inv_n, int A, int d,
-                       unsigned long long* xchg, int* err);
+                       unsigned long long* xchg, unsigned long long* gx, int ksp, int* err);
+size_t gx_bytes(int P);
 // clip_by_global_norm + tf1 Adam on a flat (all-reduced) gradient vector
 void launch_apply_adam(hipStream_t s, const float* grad, int n, float* theta, float* m, float* v,
                        float* beta_pow, const UpdateHyper& h);

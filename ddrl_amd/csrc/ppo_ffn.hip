@@ -25,22 +25,33 @@
 
 // Workgroup geometry: NW waves (8 = two per SIMD with one 16-row tile each; the A = 8
 // kernels use 4 waves with two tiles each, their per-wave head partials would not fit LDS).
-template <int NW>
+// Row split (KSP = 2): each branch runs on two workgroups that take 64 rows of the minibatch
+// each (one 16-row tile per wave, four waves) and swap their partial gradients every step
+// through tagged 8-byte granules; both then hold the same summed gradient and run the same
+// clip + Adam, so their weight images stay bit-identical.
+template <int NW, int ROWS>
 struct Geo {
   static constexpr int NT = 64 * NW;
-  static constexpr int RT = DDRL_MB / (16 * NW);   // 16-row tiles per wave
+  static constexpr int RT = ROWS / (16 * NW);      // 16-row tiles per wave
   static constexpr int NS1 = 16 / NW;              // dW2 tile slots per wave (16 tiles)
   static constexpr int NS2 = (12 + NW - 1) / NW;   // dW1 tile slots per wave (<= 12 tiles)
 };
-__host__ __device__ constexpr int waves_for(int A) { return A == 8 ? 4 : 8; }
+__host__ __device__ constexpr int waves_for(int A, int ksp) { return ksp == 2 ? 4 : (A == 8 ? 4 : 8); }
+// value pairs per lane of the partner exchange: small params + stats (padded to a pair),
+// then two per owned dW tile
+__host__ __device__ constexpr int gx_pairs(int OB, int NW) {
+  return ((64 * OB + OB + 128 + 64 * NW - 1) / (64 * NW) + 2) / 2 + 2 * (16 / NW + (12 + NW - 1) / NW);
+}
+#define GX_MAX_PAIRS 20
 
 struct UpdateBatch {
   const UpdateArgs* a;   // device array, one entry per policy
   UpdateHyper h;
   int nrows;             // rows per minibatch handled here (<= 128)
   float inv_n;           // 1 / sgd_minibatch_size (global minibatch)
-  unsigned long long* xchg;  // [P][2 branches][2 parities] tagged norm^2 granules
-  int* err;              // set to 1 if a norm exchange timed out
+  unsigned long long* xchg;  // [P][2 branches][KSP][2 parities] tagged norm^2 granules
+  unsigned long long* gx;    // [P][2 branches][KSP][2 parities][GX_MAX_PAIRS][256 lanes][2] partial-gradient granules
+  int* err;              // set to 1 if an exchange timed out
 };
 
 // Per-branch view of the flat (Keras-order) parameter vector.
@@ -98,12 +109,12 @@ struct RowData {
 // reads then start in 16 different banks); the pad chunk repeats the row's last chunk.
 // Issued by waves 0 .. NW-2: the last wave keeps its vector-memory counter free for the
 // norm exchange (an early partner poll would otherwise wait for the gathers too).
-template <int NW>
+template <int NW, int ROWS>
 __device__ __forceinline__ void issue_rows(const float* rec, int stride, int cpr, int cpr_l, const int* idxb,
                                            float* stg) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (w == NW - 1) return;
-  const int nchunk = DDRL_MB * cpr_l;
+  const int nchunk = ROWS * cpr_l;
   const float inv = 1.f / (float)cpr_l;
   for (int base = 64 * w; base < nchunk; base += 64 * (NW - 1)) {   // wave-uniform
     const int g = base + lane;
@@ -150,13 +161,17 @@ __device__ __forceinline__ void load_row(const float* stg, int stg_stride, const
 
 // Per-step learner statistics from the per-wave partial sums red[w * 8 + k]: policy
 // workgroup -> policy_loss, kl, entropy; value workgroup -> vf_loss, vf_explained_var.
-template <bool POL, int NSTAT, int NW>
+template <bool POL, int NSTAT, int NW, int KSP>
 __device__ __forceinline__ void write_stats(float* so, const float* red, float n) {
   float sv[NSTAT];
 #pragma unroll
   for (int k = 0; k < NSTAT; ++k) {
-    sv[k] = 0.f;
-    for (int i = 0; i < NW; ++i) sv[k] += red[i * 8 + k];
+    if constexpr (KSP == 2) {
+      sv[k] = red[96 + k];   // both workgroups' sums, combined at the exchange
+    } else {
+      sv[k] = 0.f;
+      for (int i = 0; i < NW; ++i) sv[k] += red[i * 8 + k];
+    }
   }
   if constexpr (POL) {
     gst(so + 1, sv[0] / n); gst(so + 3, sv[1] / n); gst(so + 4, sv[2] / n);
@@ -182,7 +197,7 @@ __device__ __forceinline__ int perm_slot(const UpdateArgs& U, int step) {
 // Diagnostic build only (-DDDRL_STAMPS): per-phase s_memtime cycle counts of wave 0 of each
 // workgroup, accumulated over the steps of one launch; no stamp executes in the real build.
 #ifdef DDRL_STAMPS
-__device__ unsigned long long g_stamps[16][16];
+__device__ unsigned long long g_stamps[32][16];
 #define STAMP_INIT unsigned long long st_prev = __builtin_amdgcn_s_memtime(), st_acc[16] = {0};
 #define STAMP(k) do { if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[k] += t_ - st_prev; st_prev = t_; } } while (0)
 #define STAMP_DONE do { if (tid == 0) for (int k_ = 0; k_ < 16; ++k_) g_stamps[blockIdx.x][k_] = st_acc[k_]; } while (0)
@@ -195,9 +210,50 @@ extern "C" int ddrl_diag_stamps(unsigned long long* host) {
 #define STAMP_DONE
 #endif
 
-template <int A, int KS1, int OB, bool POL, int NW>
-__device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBatch& ub, float* lds, int p) {
-  constexpr int NT = Geo<NW>::NT, RT = Geo<NW>::RT, NS1 = Geo<NW>::NS1, NS2 = Geo<NW>::NS2;
+// Partner exchange of the row split: 16-byte granules {value, tag, value, tag} (each 8-byte
+// half carries the step tag, so a half is valid exactly when its tag matches: no fence),
+// written by one sc1 (write-through) buffer store and read by one sc1 buffer load; the
+// outboxes are double buffered by step parity and cleared before each launch.  Pair j of
+// lane l sits at box[(j * 256 + l) * 16 bytes] (coalesced per pair).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gx_rsrc(unsigned long long* box) {
+  return __builtin_amdgcn_make_buffer_rsrc(box, 0, GX_MAX_PAIRS * 256 * 16, 0x00020000);
+}
+__device__ __forceinline__ void gx_put(__amdgpu_buffer_rsrc_t r, int j, float v0, float v1, unsigned tag) {
+  const v4u g = {__float_as_uint(v0), tag, __float_as_uint(v1), tag};
+  __builtin_amdgcn_raw_buffer_store_b128(g, r, (j * 256 + (int)threadIdx.x) * 16, 0, 16);
+}
+// The partner's NP pairs of this lane: all loads in flight, re-polled until every tag
+// matches; bounded (a timeout flags err and returns zeros).
+template <int NP>
+__device__ __forceinline__ void gx_get(__amdgpu_buffer_rsrc_t r, unsigned tag, float* out, int* err) {
+  v4u g[NP];
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+#pragma unroll
+    for (int j = 0; j < NP; ++j) g[j] = __builtin_amdgcn_raw_buffer_load_b128(r, (j * 256 + (int)threadIdx.x) * 16, 0, 16);
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) ok = ok && g[j][1] == tag && g[j][3] == tag;
+    if (ok) break;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 300000000ull) {   // 3 s at 100 MHz
+      atomicExch(err, 1);
+#pragma unroll
+      for (int j = 0; j < NP; ++j) g[j] = v4u{0u, 0u, 0u, 0u};
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    out[2 * j] = __uint_as_float(g[j][0]);
+    out[2 * j + 1] = __uint_as_float(g[j][2]);
+  }
+}
+
+template <int A, int KS1, int OB, bool POL, int NW, int KSP>
+__device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBatch& ub, float* lds, int p, int kq) {
+  constexpr int ROWS = DDRL_MB / KSP;
+  constexpr int NT = Geo<NW, ROWS>::NT, RT = Geo<NW, ROWS>::RT, NS1 = Geo<NW, ROWS>::NS1, NS2 = Geo<NW, ROWS>::NS2;
   const UpdateHyper& H = ub.h;
   const int d = U.d;
   const FfnOffsets of = ffn_offsets(d, A);
@@ -207,15 +263,19 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   constexpr int NSLOT = (NSB + NT - 1) / NT;
   constexpr int NSTAT = POL ? 3 : 5;
   constexpr int NTS = NS1 + NS2;
+  constexpr int NP0 = (NSLOT + 2) / 2;              // exchange pairs: small params + stats,
+  constexpr int NP = NP0 + 2 * NTS;                  // then the owned dW tiles (KSP = 2)
+  static_assert(KSP == 1 || (NT == 256 && NP == gx_pairs(OB, NW) && NP <= GX_MAX_PAIRS), "exchange pairs");
 
   NetLds W;
   stage_branch<OB>(U.theta, d, bo, lds, W);
-  float* bufA = lds + BRANCH_LDS_FLOATS;    // feature-major [64][FM_LD]: H1, then X
-  float* bufB = bufA + 64 * FM_LD;          // feature-major [64][FM_LD]: dZ2, then dZ1
-  float* Pb = bufB + 64 * FM_LD;            // [NW][NSB] per-wave partial small grads
+  constexpr int LD = ROWS + 8;              // feature-major image stride
+  float* bufA = lds + BRANCH_LDS_FLOATS;    // feature-major [64][LD]: H1, then X
+  float* bufB = bufA + 64 * LD;             // feature-major [64][LD]: dZ2, then dZ1
+  float* Pb = bufB + 64 * LD;               // [NW][NSB] per-wave partial small grads
   float* red = Pb + NW * NSB;               // [NW][8] row-stat partials, [64..] scalars
   int* idxb = reinterpret_cast<int*>(red + 128);   // [128] record rows of the next step
-  float* stg = red + 256;                   // [128][stride] records of the next step (16 B aligned)
+  float* stg = red + 256;                   // [ROWS][stride] records of the next step (16 B aligned)
   const int stride = U.lay.stride, cpr = stride >> 2, cpr_l = stg_chunks(stride, A);
 
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, q = lane >> 4, w = tid >> 6;
@@ -223,8 +283,8 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   bool row_ok[RT];
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
-    row_l[t] = 16 * RT * w + 16 * t + c;
-    row_ok[t] = row_l[t] < ub.nrows;
+    row_l[t] = 16 * RT * w + 16 * t + c;               // row of this workgroup's share
+    row_ok[t] = ROWS * kq + row_l[t] < ub.nrows;
   }
 
   // ---- optimizer state of the parameters this lane owns ----
@@ -246,6 +306,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       const int pidx = (i < NS1 ? bo.w2 : bo.w1) + f * 64 + o;
       mt[i][r] = ok ? U.m[pidx] : 0.f;
       vt4[i][r] = ok ? U.v[pidx] : 0.f;
+
     }
   }
   float ms[NSLOT], vs[NSLOT];
@@ -273,14 +334,18 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   const int last = U.max_steps >= 0 ? min(total_steps, U.step0 + U.max_steps) : total_steps;
   RowData<A, RT> cur;
   // records of step0 -> stg, row indices of step0 + 1 -> idxb, of step0 + 2 -> nxt
-  const int tr = tid < ub.nrows ? tid : 0;
-  if (tid < DDRL_MB) idxb[tid] = U.step0 < last && tid < ub.nrows ? row_index(U, U.step0, tr, true) : 0;
+  // minibatch row of this lane's staging slot (tid < ROWS)
+  const int gr = ROWS * kq + tid;
+  const bool gok = tid < ROWS && gr < ub.nrows;
+  if (tid < ROWS) idxb[tid] = U.step0 < last && gok ? row_index(U, U.step0, gr, true) : 0;
   __syncthreads();
-  if (U.step0 < last) issue_rows<NW>(U.rec, stride, cpr, cpr_l, idxb, stg);
+  if (U.step0 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, idxb, stg);
   wait_vmcnt0();
   __syncthreads();
-  if (tid < DDRL_MB) idxb[tid] = U.step0 + 1 < last && tid < ub.nrows ? row_index(U, U.step0 + 1, tr, true) : 0;
-  int nxt = tid < DDRL_MB && U.step0 + 2 < last && tid < ub.nrows ? row_index(U, U.step0 + 2, tr, true) : 0;
+  if (tid < ROWS) idxb[tid] = U.step0 + 1 < last && gok ? row_index(U, U.step0 + 1, gr, true) : 0;
+  int nxt = U.step0 + 2 < last && gok ? row_index(U, U.step0 + 2, gr, true) : 0;
+  // partner exchange slots: mine / the other row half of this branch, by step parity
+  const size_t gx_branch = ((size_t)p * 2 + (POL ? 0 : 1)) * KSP;
   __syncthreads();
 
   STAMP_INIT
@@ -359,8 +424,8 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     }
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
-      store_act_fm(bufA, RT * w + t, h1[t]);
-      store_act_fm(bufB, RT * w + t, dz[t]);
+      store_act_fm<LD>(bufA, RT * w + t, h1[t]);
+      store_act_fm<LD>(bufB, RT * w + t, dz[t]);
     }
     STAMP(3);
 #ifndef DDRL_ABL_NO_L2BWD
@@ -383,33 +448,67 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     STAMP(4);
     __syncthreads();                                     // #1: H1, dZ2, partials visible
     STAMP(5);
+    const unsigned gtag = (unsigned)step + 1u;
+    const size_t gx_box = (size_t)GX_MAX_PAIRS * 256 * 2;   // granules per outbox
+    const __amdgpu_buffer_rsrc_t gx_mine = gx_rsrc(ub.gx + ((gx_branch + kq) * 2 + (step & 1)) * gx_box);
+    float gs[NSLOT];
+    float st_own = 0.f;
+    if constexpr (KSP == 2) {
+      // small-parameter partials and this half's loss statistics go out first
+      float v0[2 * NP0];
+#pragma unroll
+      for (int k = 0; k < 2 * NP0; ++k) v0[k] = 0.f;
+#pragma unroll
+      for (int k = 0; k < NSLOT; ++k) {
+        const int e = tid + NT * k;
+        float sm = 0.f;
+        if (e < NSB)
+          for (int i = 0; i < NW; ++i) sm += Pb[i * NSB + e];
+        gs[k] = sm;
+        v0[k] = sm;
+      }
+      if (tid < NSTAT)
+        for (int i = 0; i < NW; ++i) st_own += red[i * 8 + tid];
+      v0[NSLOT] = st_own;
+#pragma unroll
+      for (int j = 0; j < NP0; ++j) gx_put(gx_mine, j, v0[2 * j], v0[2 * j + 1], gtag);
+    }
     floatx4 gt[NTS];
 #ifndef DDRL_ABL_NO_DW2   // ablation builds (timing only): skip a phase
-    dw_tiles_fm<DDRL_MB, NS1>(bufA, bufB, tfa, w & 3, gt);   // dW2 tiles of this wave
+    dw_tiles_fm<ROWS, NS1>(bufA, bufB, tfa, w & 3, gt);   // dW2 tiles of this wave
 #else
     for (int i = 0; i < NS1; ++i) gt[i] = splat4(0.f);
 #endif
+    if constexpr (KSP == 2) {
+#pragma unroll
+      for (int i = 0; i < NS1; ++i) {
+        gx_put(gx_mine, NP0 + 2 * i, gt[i][0], gt[i][1], gtag);
+        gx_put(gx_mine, NP0 + 2 * i + 1, gt[i][2], gt[i][3], gtag);
+      }
+    }
     STAMP(6);
     __syncthreads();                                     // #2: dW2 operands consumed
     STAMP(7);
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
-      store_act_fm(bufB, RT * w + t, h2[t]);
+      store_act_fm<LD>(bufB, RT * w + t, h2[t]);
 #pragma unroll
-      for (int s = 0; s < 12; ++s) bufA[(4 * s + q) * FM_LD + row_l[t]] = cur.x[t][s];
+      for (int s = 0; s < 12; ++s) bufA[(4 * s + q) * LD + row_l[t]] = cur.x[t][s];
     }
     __syncthreads();                                     // #3: X, dZ1 visible
     STAMP(8);
     // ---- prefetch: the records of step + 1 land in stg (LDS-DMA) while the dW1 tiles, the
-    //      norm exchange and Adam run; every lane has read its rows of this step (sync #1)
+    //      norm exchange and Adam run; every lane has read its rows of this step (sync #1).
+    //      The row split issues them after its partner exchange instead: vmcnt retires in
+    //      order, so the exchange loads would otherwise wait for the gathers.
 #ifndef DDRL_ABL_NO_PREFETCH
-    if (step + 1 < last) issue_rows<NW>(U.rec, stride, cpr, cpr_l, idxb, stg);
+    if (KSP == 1 && step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, idxb, stg);
 #endif
     // the exchange lane (wave NW-1, which issued no gathers) polls the partner's granule
     // early: when the other branch is ahead, its norm^2 is already there at the exchange
     const int xlane = 64 * (NW - 1);
-    unsigned long long* const xmine = ub.xchg + ((size_t)p * 2 + (POL ? 0 : 1)) * 2 + (step & 1);
-    unsigned long long* const xother = ub.xchg + ((size_t)p * 2 + (POL ? 1 : 0)) * 2 + (step & 1);
+    unsigned long long* const xmine = ub.xchg + (((size_t)p * 2 + (POL ? 0 : 1)) * KSP + kq) * 2 + (step & 1);
+    unsigned long long* const xother = ub.xchg + (((size_t)p * 2 + (POL ? 1 : 0)) * KSP + kq) * 2 + (step & 1);
     unsigned long long xv = 0;
     if (tid == xlane) xv = __hip_atomic_load(xother, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     STAMP(9);
@@ -423,24 +522,47 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 #ifdef DDRL_ABL_NO_DW1
       n1 = -1;
 #endif
-      if (n1 == NS2) dw_tiles_fm<DDRL_MB, NS2>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
+      if (n1 == NS2) dw_tiles_fm<ROWS, NS2>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
       else if constexpr (NS2 >= 3) {
-        if (n1 == 2) dw_tiles_fm<DDRL_MB, 2>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
-        else if (n1 == 1) dw_tiles_fm<DDRL_MB, 1>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
-      } else if (n1 == 1) dw_tiles_fm<DDRL_MB, 1>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
+        if (n1 == 2) dw_tiles_fm<ROWS, 2>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
+        else if (n1 == 1) dw_tiles_fm<ROWS, 1>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
+      } else if (n1 == 1) dw_tiles_fm<ROWS, 1>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
     }
     STAMP(10);
-    float gs[NSLOT];
+    if constexpr (KSP == 2) {
+      // last share out, then the partner's: value = mine + partner's (commutative, so
+      // both workgroups hold the same bits)
+#pragma unroll
+      for (int i = NS1; i < NTS; ++i) {
+        gx_put(gx_mine, NP0 + 2 * i, gt[i][0], gt[i][1], gtag);
+        gx_put(gx_mine, NP0 + 2 * i + 1, gt[i][2], gt[i][3], gtag);
+      }
+      float o[2 * NP];
+      gx_get<NP>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), gtag, o, ub.err);
+#pragma unroll
+      for (int k = 0; k < NSLOT; ++k) gs[k] += o[k];
+      if (tid < NSTAT) red[96 + tid] = st_own + o[NSLOT];
+#pragma unroll
+      for (int i = 0; i < NTS; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gt[i][r] += o[2 * NP0 + 4 * i + r];
+#ifndef DDRL_ABL_NO_PREFETCH
+      if (step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, idxb, stg);
+#endif
+      STAMP(14);
+    } else {
+#pragma unroll
+      for (int k = 0; k < NSLOT; ++k) {
+        const int e = tid + NT * k;
+        float sm = 0.f;
+        if (e < NSB)
+          for (int i = 0; i < NW; ++i) sm += Pb[i * NSB + e];
+        gs[k] = sm;
+      }
+    }
     float ss = 0.f;
 #pragma unroll
-    for (int k = 0; k < NSLOT; ++k) {
-      const int e = tid + NT * k;
-      float s = 0.f;
-      if (e < NSB)
-        for (int i = 0; i < NW; ++i) s += Pb[i * NSB + e];
-      gs[k] = s;
-      ss += s * s;
-    }
+    for (int k = 0; k < NSLOT; ++k) ss += gs[k] * gs[k];
 #pragma unroll
     for (int i = 0; i < NTS; ++i)
 #pragma unroll
@@ -466,7 +588,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
           U.grad_out[pidx] = gs[k];
         }
       }
-      if (U.stats && tid == 64) write_stats<POL, NSTAT, NW>(U.stats + (size_t)step * 8, red, (float)ub.nrows);
+      if (U.stats && tid == 64) write_stats<POL, NSTAT, NW, KSP>(U.stats + (size_t)step * 8, red, (float)ub.nrows);
       return;
     }
 
@@ -502,8 +624,8 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     }
     __syncthreads();                                     // #5
     STAMP(11);
-    if (U.stats && tid == 64) {   // off the critical path: wave 1, after the exchange
-      write_stats<POL, NSTAT, NW>(U.stats + (size_t)step * 8, red, (float)ub.nrows);
+    if (U.stats && tid == 64 && kq == 0) {   // off the critical path: wave 1, after the exchange
+      write_stats<POL, NSTAT, NW, KSP>(U.stats + (size_t)step * 8, red, (float)ub.nrows);
       gst(U.stats + (size_t)step * 8 + 6, red[80]);
       gst(U.stats + (size_t)step * 8 + 7, red[81]);
     }
@@ -538,6 +660,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
           vt4[i][r] = vt4[i][r] + (g * g - vt4[i][r]) * c2;
           th[i][r] = th[i][r] - (mt[i][r] * alpha) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vt4[i][r]) + H.eps);
         }
+
 #pragma unroll
       for (int k = 0; k < NSLOT; ++k) {
         const float g = gs[k] * scale;
@@ -564,13 +687,13 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     b2p = b2p * H.b2;
     STAMP(12);
     wait_vmcnt0();                                       // this wave's record gathers landed
-    if (tid < DDRL_MB) idxb[tid] = nxt;                  // row indices of step + 2
+    if (tid < ROWS) idxb[tid] = nxt;                     // row indices of step + 2
     __syncthreads();                                     // #6: weights updated, stg / idxb ready
-    if (tid < DDRL_MB) nxt = step + 3 < last && tid < ub.nrows ? row_index(U, step + 3, tr, true) : 0;
+    if (tid < ROWS) nxt = step + 3 < last && gok ? row_index(U, step + 3, gr, true) : 0;
     STAMP(13);
   }
   STAMP_DONE;
-  if (U.grad_out) return;
+  if (U.grad_out || kq != 0) return;   // the row halves hold identical state: one writes it back
 
   // ---- write back weights, optimizer state, beta powers ----
 #pragma unroll
@@ -604,46 +727,57 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   }
 }
 
-template <int A, int KS1>
-__global__ void __launch_bounds__(64 * waves_for(A)) k_update_ffn(UpdateBatch ub) {
+template <int A, int KS1, int KSP>
+__global__ void __launch_bounds__(64 * waves_for(A, KSP)) k_update_ffn(UpdateBatch ub) {
   extern __shared__ float lds[];
-  constexpr int NW = waves_for(A);
-  // policy branch of policy p = block p, value branch = block p + 8: blocks b and b + 8 are
-  // dealt to the same XCD, so the per-step norm exchange stays inside one XCD (speed only;
-  // the exchange is agent-scope either way).  Blocks P..7 have no work.
+  constexpr int NW = waves_for(A, KSP);
+  // block b = p + 8 j, j = KSP branch + kq (branch 0 = policy, kq = row half): the blocks of
+  // one policy are dealt to the same XCD (b mod 8), so its per-step exchanges stay inside
+  // one XCD (speed only; they are agent-scope either way).  Blocks with p >= P have no work.
   const int p = blockIdx.x & 7;
   if (p >= ub.h.P) return;
+  const int j = blockIdx.x >> 3, branch = j / KSP, kq = j - branch * KSP;
   const UpdateArgs U = ub.a[p];
-  if (blockIdx.x >> 3) update_loop<A, KS1, 1, false, NW>(U, ub, lds, p);
-  else update_loop<A, KS1, 2 * A, true, NW>(U, ub, lds, p);
+  if (branch) update_loop<A, KS1, 1, false, NW, KSP>(U, ub, lds, p, kq);
+  else update_loop<A, KS1, 2 * A, true, NW, KSP>(U, ub, lds, p, kq);
 }
 
 // stride: the widest record stride of the launched policies (staging buffer rows)
-static size_t update_lds_bytes(int O, int stride) {
+static size_t update_lds_bytes(int O, int stride, int ksp) {
   const int nsb = 64 * O + O + 128;
-  return (size_t)(BRANCH_LDS_FLOATS + 2 * 64 * FM_LD + waves_for(O / 2) * nsb + 256 +
-                  DDRL_MB * 4 * stg_chunks(stride, O / 2)) * 4;
+  const int nw = waves_for(O / 2, ksp);
+  return (size_t)(BRANCH_LDS_FLOATS + 2 * 64 * (DDRL_MB / ksp + 8) + nw * nsb + 256 +
+                  (DDRL_MB / ksp) * 4 * stg_chunks(stride, O / 2)) * 4;
 }
 
 template <int A, int KS1>
-static void launch_update_t(hipStream_t s, const UpdateBatch& ub, int P, int stride) {
-  hipLaunchKernelGGL((k_update_ffn<A, KS1>), dim3(8 + P), dim3(64 * waves_for(A)), update_lds_bytes(2 * A, stride), s,
-                     ub);
+static void launch_update_t(hipStream_t s, const UpdateBatch& ub, int P, int stride, int ksp) {
+  if (ksp == 2)
+    hipLaunchKernelGGL((k_update_ffn<A, KS1, 2>), dim3(24 + P), dim3(64 * waves_for(A, 2)),
+                       update_lds_bytes(2 * A, stride, 2), s, ub);
+  else
+    hipLaunchKernelGGL((k_update_ffn<A, KS1, 1>), dim3(8 + P), dim3(64 * waves_for(A, 1)),
+                       update_lds_bytes(2 * A, stride, 1), s, ub);
 }
 
 void launch_update_ffn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHyper& h, int nrows, float inv_n,
-                       int A, int d, unsigned long long* xchg, int* err) {
+                       int A, int d, unsigned long long* xchg, unsigned long long* gx, int ksp, int* err) {
   UpdateBatch ub;
   ub.a = ua_dev;
   ub.h = h;
   ub.nrows = nrows;
   ub.inv_n = inv_n;
   ub.xchg = xchg;
+  ub.gx = gx;
   ub.err = err;
-  (void)hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * 4 * h.P, s);
+  // step tags restart at 1 every launch: clear the previous launch's granules
+  (void)hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * 4 * ksp * h.P, s);
+  if (ksp == 2) (void)hipMemsetAsync(gx, 0, gx_bytes(h.P), s);
   const int stride = (d + 3 * A + 5 + 3) & ~3;   // RecLayout stride of the widest policy (capi make_layout)
-  DDRL_DISPATCH_A_KS1(A, d, launch_update_t, s, ub, h.P, stride);
+  DDRL_DISPATCH_A_KS1(A, d, launch_update_t, s, ub, h.P, stride, ksp);
 }
+
+size_t gx_bytes(int P) { return sizeof(unsigned long long) * (size_t)P * 2 * 2 * 2 * GX_MAX_PAIRS * 256 * 2; }
 
 // ------------------------------------------------------------------------------------
 // DDP apply: tf.clip_by_global_norm + tf1 Adam on an all-reduced flat gradient.

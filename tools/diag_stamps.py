@@ -33,15 +33,18 @@ for it in range(2):
     ctx.ppo_update(0xF, sh, pe, [0.2] * 4)
     ctx.synchronize()
     dt = time.perf_counter() - t0
-st = (ctypes.c_ulonglong * (16 * 16))()
+st = (ctypes.c_ulonglong * (32 * 16))()
 assert N.load().ddrl_diag_stamps(st) == 0
-a = np.array(st, dtype=np.float64).reshape(16, 16)[[0, 8], :14] / steps
-names = ["fwd", "loss", "dpp head/bias", "head bwd+db2+stores", "layer2 bwd+db1", "sync#1",
-         "dW2 tiles", "sync#2", "X/dZ1 stores + sync#3", "prefetch issue", "dW1 tiles",
-         "norm+exchange", "adam", "sync#6"]
+split = os.environ.get("DDRL_UPDATE_SPLIT", "2") != "1"
+blocks = [0, 8, 16] if split else [0, 8]
+labels = ["policy rows 0-63", "policy rows 64-127", "value rows 0-63"] if split else ["policy", "value"]
+a = np.array(st, dtype=np.float64).reshape(32, 16)[blocks, :15] / steps
+names = ["fwd", "loss", "dpp head/bias", "head bwd+db2+stores", "layer2 bwd+db1", "sync#1 (+gs/stats out)",
+         "dW2 tiles (+out)", "sync#2", "X/dZ1 stores + sync#3", "prefetch issue", "dW1 tiles",
+         "norm exchange", "adam", "sync#6", "partner exchange (split)"]
 print(f"steps {steps}, {dt / steps * 1e6:.2f} us/step wall")
-for wg in (0, 1):
+for wg in range(len(blocks)):
     tot = a[wg].sum()
-    print(("policy" if wg == 0 else "value ") + f" WG: {tot:.0f} cycles/step")
+    print(f"{labels[wg]} WG: {tot:.0f} cycles/step")
     for k, nm in enumerate(names):
         print(f"   {nm:45s} {a[wg, k]:8.0f}  {100 * a[wg, k] / tot:5.1f}%")
