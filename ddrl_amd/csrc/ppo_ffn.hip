@@ -5,7 +5,7 @@
 // branches share no parameters, so each workgroup computes its own gradients and runs Adam
 // on its own parameters; the only coupling is tf.clip_by_global_norm, which needs the
 // squared norm over ALL variables: every step the two workgroups swap their partial
-// squared norms through one tagged 8-byte granule each (sc1 store / sc1 poll, slots double
+// squared norms through one tagged 8-byte granule each (plain store / sc1 poll, slots double
 // buffered by step parity, zeroed by a memset before every launch, spins bounded).
 //
 // Per minibatch step (RLlib TrainTFMultiGPU: row = shuffle[perm[e][b] * 128 + i]):
@@ -18,6 +18,7 @@
 //   gradient GEMMs (16x16 tiles, K = 128 rows); per-wave tile ownership;
 //   global-norm clip; tf1 Adam (ApplyAdam) with m / v held in registers by the owning
 //   lane and the weights updated in place in the LDS image.
+#include <atomic>
 #include "common.h"
 #include "kernels.h"
 #include "ffn.h"
@@ -52,7 +53,13 @@ struct UpdateBatch {
   unsigned long long* xchg;  // [P][2 branches][KSP][2 parities] tagged norm^2 granules
   unsigned long long* gx;    // [P][2 branches][KSP][2 parities][GX_MAX_PAIRS][256 lanes][2] partial-gradient granules
   int* err;              // set to 1 if an exchange timed out
+  unsigned epoch;        // launch counter (12 bits, never 0): high bits of every exchange tag
 };
+// Exchange tag of a step: the launch epoch above the step count, so a granule line some
+// cache still holds from an earlier launch can never carry a tag of this one.
+__device__ __forceinline__ unsigned xchg_tag(unsigned epoch, int step) {
+  return (epoch << 20) | (((unsigned)step + 1u) & 0xfffffu);
+}
 
 // Per-branch view of the flat (Keras-order) parameter vector.
 struct BranchOff { int w1, b1, w2, b2, wo, bo; };
@@ -215,12 +222,59 @@ extern "C" int ddrl_diag_stamps(unsigned long long* host) {
 // written by one sc1 (write-through) buffer store and read by one sc1 buffer load; the
 // outboxes are double buffered by step parity and cleared before each launch.  Pair j of
 // lane l sits at box[(j * 256 + l) * 16 bytes] (coalesced per pair).
+// Cache policy of the exchange (gfx950 CPol bits: sc0 = 1, nt = 2, sc1 = 16).  The four
+// workgroups of a policy share one XCD and hence one L2 (blocks b, b + 8, ... are dealt to
+// XCD b mod 8; tools/xchg_bench.hip prints the placement).  Plain stores write through the
+// per-CU L1 into that L2 and stay there; the poller's sc1 (device-scope) loads miss its own
+// L1.  Measured one-hop latency (tools/xchg_bench.hip, MI355X): plain store / sc1 load
+// 0.24 us, sc1 store / sc1 load 0.50 us (the sc1 store writes through to memory), sc0 loads
+// never see the partner (they hit the stale L1 line).
+#ifndef DDRL_GX_ST
+#define DDRL_GX_ST 0
+#endif
+#ifndef DDRL_GX_LD
+#define DDRL_GX_LD 16
+#endif
+#ifndef DDRL_GX_INV
+#define DDRL_GX_INV 0
+#endif
+__device__ __forceinline__ void xchg_inv_l1() {
+#if DDRL_GX_INV
+  asm volatile("buffer_inv sc0" ::: "memory");
+#endif
+}
+// Once any exchange has waited this long (100 MHz ticks), the waiter also polls the error
+// word, so one timed-out exchange ends every later wait at once instead of each one
+// spinning to its own timeout.
+#define XCHG_SLOW_TICKS 20000ull        // 200 us
+#define XCHG_TIMEOUT_TICKS 300000000ull // 3 s
+__device__ __forceinline__ bool xchg_abandon(unsigned long long t0, int* err) {
+  const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
+  if (dt < XCHG_SLOW_TICKS) return false;
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return true;
+  if (dt > XCHG_TIMEOUT_TICKS) { atomicExch(err, 1); return true; }
+  return false;
+}
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t gx_rsrc(unsigned long long* box) {
   return __builtin_amdgcn_make_buffer_rsrc(box, 0, GX_MAX_PAIRS * 256 * 16, 0x00020000);
 }
 __device__ __forceinline__ void gx_put(__amdgpu_buffer_rsrc_t r, int j, float v0, float v1, unsigned tag) {
   const v4u g = {__float_as_uint(v0), tag, __float_as_uint(v1), tag};
-  __builtin_amdgcn_raw_buffer_store_b128(g, r, (j * 256 + (int)threadIdx.x) * 16, 0, 16);
+  __builtin_amdgcn_raw_buffer_store_b128(g, r, (j * 256 + (int)threadIdx.x) * 16, 0, DDRL_GX_ST);
+}
+// Norm granule (8 bytes: tag << 32 | value), one 64-bit access each way, same policy.
+__device__ __forceinline__ void xchg_store(unsigned long long* g, unsigned long long v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(g, 0, 8, 0x00020000);
+  typedef unsigned v2u_t __attribute__((ext_vector_type(2)));
+  const v2u_t x = {(unsigned)v, (unsigned)(v >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b64(x, r, 0, 0, DDRL_GX_ST);
+}
+__device__ __forceinline__ unsigned long long xchg_load(unsigned long long* g) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(g, 0, 8, 0x00020000);
+  typedef unsigned v2u_t __attribute__((ext_vector_type(2)));
+  xchg_inv_l1();
+  const v2u_t x = __builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, DDRL_GX_LD);
+  return ((unsigned long long)x[1] << 32) | x[0];
 }
 // The partner's NP pairs of this lane: all loads in flight, re-polled until every tag
 // matches; bounded (a timeout flags err and returns zeros).
@@ -229,14 +283,14 @@ __device__ __forceinline__ void gx_get(__amdgpu_buffer_rsrc_t r, unsigned tag, f
   v4u g[NP];
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
+    xchg_inv_l1();
 #pragma unroll
-    for (int j = 0; j < NP; ++j) g[j] = __builtin_amdgcn_raw_buffer_load_b128(r, (j * 256 + (int)threadIdx.x) * 16, 0, 16);
+    for (int j = 0; j < NP; ++j) g[j] = __builtin_amdgcn_raw_buffer_load_b128(r, (j * 256 + (int)threadIdx.x) * 16, 0, DDRL_GX_LD);
     bool ok = true;
 #pragma unroll
     for (int j = 0; j < NP; ++j) ok = ok && g[j][1] == tag && g[j][3] == tag;
     if (ok) break;
-    if (__builtin_amdgcn_s_memrealtime() - t0 > 300000000ull) {   // 3 s at 100 MHz
-      atomicExch(err, 1);
+    if (xchg_abandon(t0, err)) {
 #pragma unroll
       for (int j = 0; j < NP; ++j) g[j] = v4u{0u, 0u, 0u, 0u};
       break;
@@ -448,7 +502,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     STAMP(4);
     __syncthreads();                                     // #1: H1, dZ2, partials visible
     STAMP(5);
-    const unsigned gtag = (unsigned)step + 1u;
+    const unsigned gtag = xchg_tag(ub.epoch, step);
     const size_t gx_box = (size_t)GX_MAX_PAIRS * 256 * 2;   // granules per outbox
     const __amdgpu_buffer_rsrc_t gx_mine = gx_rsrc(ub.gx + ((gx_branch + kq) * 2 + (step & 1)) * gx_box);
     float gs[NSLOT];
@@ -510,7 +564,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     unsigned long long* const xmine = ub.xchg + (((size_t)p * 2 + (POL ? 0 : 1)) * KSP + kq) * 2 + (step & 1);
     unsigned long long* const xother = ub.xchg + (((size_t)p * 2 + (POL ? 1 : 0)) * KSP + kq) * 2 + (step & 1);
     unsigned long long xv = 0;
-    if (tid == xlane) xv = __hip_atomic_load(xother, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == xlane) xv = xchg_load(xother);
     STAMP(9);
     {
       // dW1 tiles of this wave: the valid slots are a prefix (tiles w + NW i < 4 nf1)
@@ -599,21 +653,17 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     if (tid == xlane) {
       float local = 0.f;
       for (int i = 0; i < NW; ++i) local += red[64 + i];
-      const unsigned tag = (unsigned)step + 1u;
-      __hip_atomic_store(xmine, ((unsigned long long)tag << 32) | __float_as_uint(local),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned tag = xchg_tag(ub.epoch, step);
+      xchg_store(xmine, ((unsigned long long)tag << 32) | __float_as_uint(local));
       unsigned long long v = xv;
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 #ifdef DDRL_ABL_NO_EXCHANGE
       v = ((unsigned long long)tag << 32) | __float_as_uint(local);
 #endif
       while ((unsigned)(v >> 32) != tag) {
-        v = __hip_atomic_load(xother, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v = xchg_load(xother);
         if ((unsigned)(v >> 32) == tag) break;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 300000000ull) {   // 3 s at 100 MHz
-          atomicExch(ub.err, 1);
-          break;
-        }
+        if (xchg_abandon(t0, ub.err)) break;
         __builtin_amdgcn_s_sleep(1);
       }
       const float partner = __uint_as_float((unsigned)(v & 0xffffffffu));
@@ -770,7 +820,9 @@ void launch_update_ffn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHype
   ub.xchg = xchg;
   ub.gx = gx;
   ub.err = err;
-  // step tags restart at 1 every launch: clear the previous launch's granules
+  static std::atomic<unsigned> launches{0};
+  ub.epoch = launches.fetch_add(1, std::memory_order_relaxed) % 4095u + 1u;
+  // clear the previous launch's granules (the epoch in every tag keeps them apart anyway)
   (void)hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * 4 * ksp * h.P, s);
   if (ksp == 2) (void)hipMemsetAsync(gx, 0, gx_bytes(h.P), s);
   const int stride = (d + 3 * A + 5 + 3) & ~3;   // RecLayout stride of the widest policy (capi make_layout)

@@ -1,8 +1,11 @@
 """Ablation timing of the fused update kernel: builds diagnostic variants that each skip
 one phase (results are wrong; only the per-step time matters) and reports us/step.
 
-    python tools/ablate.py build        # in the container (hipcc)
-    python tools/ablate.py run [envs]   # on the GPU box
+    python tools/ablate.py build [variants...]        # in the container (hipcc)
+    python tools/ablate.py run [envs] [variants...]   # on the GPU box
+
+A variant is a comma-separated list of macro definitions (`DDRL_ABL_NO_DW2`,
+`DDRL_GX_ST=16,DDRL_GX_LD=16`); "" is the baseline build.
 """
 import os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -13,22 +16,26 @@ VARIANTS = ["", "DDRL_ABL_NO_DW2", "DDRL_ABL_NO_DW1", "DDRL_ABL_NO_L2BWD", "DDRL
 def paths(v):
     from ddrl_amd import native as N
     d = os.path.dirname(N.LIB_PATH)
-    tag = v.replace("DDRL_ABL_", "").lower() or "base"
+    tag = "".join(ch if ch.isalnum() else "_" for ch in v.replace("DDRL_ABL_", "").replace("DDRL_", "")).lower() or "base"
     return os.path.join(d, f"libddrl_hip_abl_{tag}.so"), os.path.join(d, f"_build_abl_{tag}")
 
 
-def build():
+def flags(v):
+    return [f"-D{x}" for x in v.split(",") if x]
+
+
+def build(variants):
     from ddrl_amd import build as B
-    for v in VARIANTS:
+    for v in variants:
         lib, bd = paths(v)
-        print(B.build(extra_flags=[f"-D{v}"] if v else [], lib=lib, build_dir=bd), flush=True)
+        print(B.build(extra_flags=flags(v), lib=lib, build_dir=bd), flush=True)
 
 
-def run(n):
+def run(n, variants):
     import subprocess
-    for v in VARIANTS:
+    for v in variants:
         lib, _ = paths(v)
-        out = subprocess.run([sys.executable, __file__, "one", lib, str(n)], capture_output=True, text=True)
+        out = subprocess.run([sys.executable, __file__, "one", lib, str(n)], capture_output=True, text=True, timeout=180)
         print(f"{v or 'baseline':28s} {out.stdout.strip()} {out.stderr.strip()[-200:]}", flush=True)
 
 
@@ -63,8 +70,8 @@ def one(lib, n):
 
 if __name__ == "__main__":
     if sys.argv[1] == "build":
-        build()
+        build(sys.argv[2:] or VARIANTS)
     elif sys.argv[1] == "run":
-        run(int(sys.argv[2]) if len(sys.argv) > 2 else 512)
+        run(int(sys.argv[2]) if len(sys.argv) > 2 else 512, sys.argv[3:] or VARIANTS)
     else:
         one(sys.argv[2], int(sys.argv[3]))
