@@ -278,8 +278,10 @@ def main():
     else:
         kernel = (f"k_update_ffn<{A}, {ks1}> grad + RCCL all-reduce + k_apply_adam per step" if ddp else
                   "k_update_ffn (fused PPO minibatch SGD, one launch per iteration)")
-        # the fused launch keeps 2 workgroups (policy / value branch) per policy, one per CU
-        active_cus = 2 * P
+        # the fused launch keeps 2 workgroups (policy / value branch) per policy, one per CU,
+        # times the row split (DDRL_UPDATE_SPLIT, default 2; the data-parallel grad launch is unsplit)
+        split = 1 if ddp else (1 if os.environ.get("DDRL_UPDATE_SPLIT", "2") == "1" else 2)
+        active_cus = 2 * P * split
         model = f"{P} {'shared' if P == 1 else 'independent'} fcnet 2x64 polic{'y' if P == 1 else 'ies'} (d={d}, A={A})"
     # algorithmic HBM bytes: each minibatch row's record fields read once per branch
     # (policy: obs, action, old logits, logp, adv; value: obs, vf, vt) + its shuffle index
@@ -314,7 +316,7 @@ def main():
             "kernel": kernel,
             "bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved_tf / PEAK_FP32_TFLOPS,
-            "traffic": None if (gnn or ddp) else pmc_traffic(f"k_update_ffn<{A}, {ks1}>", steps_per_policy * P),
+            "traffic": None if (gnn or ddp) else pmc_traffic(f"k_update_ffn<{A}, {ks1},", steps_per_policy * P),
             "algorithmic_flops_per_launch": flops_launch,
             "algorithmic_bytes_per_launch": rec_bytes_launch,
             "active_cus": active_cus,

@@ -11,4 +11,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/t
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $OUT/pmc_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $OUT/pmc_write.log 2>&1
 cd $R
+# the bench reports traffic from profiles/r01/pmc_update.json: refresh it from these passes
+python3 tools/pmc_summary.py $OUT > $OUT/pmc_update.json
+cp $OUT/pmc_update.json $R/profiles/r01/pmc_update.json
 timeout -k 10 400 python3 bench.py > $OUT/bench_default.log 2>&1
