@@ -95,7 +95,8 @@ static RecLayout make_layout(const ddrl_cfg& cfg, int d) {
   L.adv = L.vf + 1;
   L.vt = L.adv + 1;
   L.rew = L.vt + 1;
-  L.stride = (L.rew + 1 + 3) & ~3;
+  L.cid = cfg.leg_coupling ? L.rew + 1 : -1;   // "cup": the row's leg index (coupling row)
+  L.stride = ((cfg.leg_coupling ? L.cid : L.rew) + 1 + 3) & ~3;
   return L;
 }
 
@@ -117,6 +118,9 @@ static int validate(const ddrl_cfg& c) {
   if (c.model_kind == DDRL_MODEL_GNN && (c.n_policies != 1 || c.n_agents != 4 || c.obs_dim[0] != 19))
     return fail("gnn requires one shared leg policy, 4 agents and 19 features per node");
   if (c.model_kind == DDRL_MODEL_GNN && c.act_dim != 2) return fail("gnn kernels are built for act_dim 2");
+  if (c.leg_coupling && (c.model_kind != DDRL_MODEL_FFN || c.act_dim != 2 || c.n_policies != 1 || c.n_agents != 4 ||
+                          c.obs_dim[0] > 20))
+    return fail("leg_coupling (\"cup\") requires the fcnet model, one shared leg policy, 4 agents, act_dim 2 and obs_dim <= 20");
   if (c.policy_filter && c.model_kind != DDRL_MODEL_FFN)
     return fail("the per-policy MeanStdFilter is built for fcnet policies (flat observations)");
   for (int j = 0; j < c.n_agents; ++j) {
@@ -171,6 +175,7 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
     P.nb = std::max(1, P.R / g.sgd_minibatch_size);
     P.lay = make_layout(g, P.d);
     P.n_params = g.model_kind == DDRL_MODEL_FFN ? ffn_param_count(P.d, g.act_dim) : gnn_param_count(g.act_dim);
+    if (g.leg_coupling) P.n_params += 4 * g.act_dim;   // leg_coupling [4][A] after the fcnet variables
     PolicyRoute& pr = ra.pol[p];
     pr.k = P.k; pr.d = P.d;
     for (int s = 0; s < P.k; ++s) {
@@ -270,7 +275,7 @@ int ddrl_record_layout(ddrl_ctx* c, int pid, int32_t* o) {
   if (pid < 0 || pid >= c->cfg.n_policies || !o) return fail("bad policy id");
   const RecLayout& L = c->pol[pid].lay;
   o[0] = L.stride; o[1] = L.obs; o[2] = L.act; o[3] = L.logit; o[4] = L.logp;
-  o[5] = L.vf; o[6] = L.adv; o[7] = L.vt; o[8] = L.rew; o[9] = c->pol[pid].C;
+  o[5] = L.vf; o[6] = L.adv; o[7] = L.vt; o[8] = L.rew; o[9] = c->pol[pid].C; o[10] = L.cid;
   return 0;
 }
 
@@ -427,6 +432,7 @@ static ActArgs make_act(ddrl_ctx* c, int t, const float* eps, float* actions, in
     Policy& P = c->pol[p];
     aa.theta[p] = P.theta; aa.stage[p] = P.stage; aa.rec[p] = P.rec; aa.last_v[p] = P.last_v;
     aa.lay[p] = P.lay; aa.C[p] = P.C;
+    aa.cup[p] = c->cfg.leg_coupling ? P.theta + ffn_param_count(P.d, c->cfg.act_dim) : nullptr;
   }
   aa.t = t; aa.eps = eps; aa.actions = actions; aa.bootstrap = mode;
   return aa;
@@ -525,6 +531,7 @@ static UpdateArgs make_update(ddrl_ctx* c, int p, const int32_t* shuffle, const 
   u.max_steps = -1; u.step0 = 0;
   u.theta = P.theta; u.m = P.m; u.v = P.v; u.beta_pow = P.beta_pow; u.stats = P.stats;
   u.adv_norm = P.adv_norm; u.grad_out = nullptr; u.gscr = P.grad; u.kl_coeff = kl;
+  u.cup = c->cfg.leg_coupling;
   return u;
 }
 
@@ -545,14 +552,14 @@ int ddrl_ppo_update(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const 
     ++n;
   }
   if (n == 0) return 0;
-  int maxd = 0;  // KS1 instance must cover the widest policy (narrower ones are zero-padded)
-  for (int i = 0; i < n; ++i) maxd = std::max(maxd, ua[i].d);
+  int maxd = 0, maxs = 0;  // KS1 instance / staging rows must cover the widest policy
+  for (int i = 0; i < n; ++i) maxd = std::max(maxd, ua[i].d), maxs = std::max(maxs, ua[i].lay.stride);
   UpdateHyper h = make_hyper(c, n);
   // pageable source: the runtime stages (or blocks on) the copy before returning
   HIPCHK(hipMemcpyAsync(c->d_uargs, ua, sizeof(UpdateArgs) * n, hipMemcpyHostToDevice, c->stream));
   if (c->cfg.model_kind == DDRL_MODEL_FFN)
-    launch_update_ffn(c->stream, c->d_uargs, h, 128, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim, maxd,
-                      c->xchg, c->gx, c->update_split, c->err);
+    launch_update_ffn(c->stream, c->d_uargs, h, 128, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim, maxd, maxs,
+                      c->cfg.leg_coupling, c->xchg, c->gx, c->update_split, c->err);
   else
     for (int step = 0; step < c->pol[0].last_steps; ++step)   // one shared policy
       launch_step_gnn(c->stream, ua[0], h, step, 128, 1.f / c->cfg.sgd_minibatch_size, c->gnn);
@@ -594,7 +601,7 @@ int ddrl_ppo_grad(ddrl_ctx* c, int pid, const int32_t* rows, int n_rows, float k
   HIPCHK(hipMemcpyAsync(c->d_uargs, &u, sizeof(UpdateArgs), hipMemcpyHostToDevice, c->stream));
   if (c->cfg.model_kind == DDRL_MODEL_FFN)
     launch_update_ffn(c->stream, c->d_uargs, h, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim,
-                      c->pol[pid].d, c->xchg, c->gx, 1, c->err);
+                      c->pol[pid].d, c->pol[pid].lay.stride, c->cfg.leg_coupling, c->xchg, c->gx, 1, c->err);
   else
     launch_step_gnn(c->stream, u, h, 0, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->gnn);
   HIPCHK(hipGetLastError());
@@ -617,10 +624,12 @@ int ddrl_policy_forward(ddrl_ctx* c, int pid, const float* obs, const int32_t* n
   if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
   if (n < 1 || !obs || !logits || !values) return fail("bad forward arguments");
   if (c->cfg.model_kind == DDRL_MODEL_GNN && !node) return fail("gnn forward needs the node index of every row");
+  if (c->cfg.leg_coupling && !node) return fail("the \"cup\" forward needs the leg index of every row");
   Policy& P = c->pol[pid];
   ForwardArgs fa{};
   fa.theta = P.theta; fa.x = obs; fa.node = node; fa.n = n; fa.d = P.d; fa.A = c->cfg.act_dim;
   fa.logits = logits; fa.values = values;
+  fa.cup = c->cfg.leg_coupling ? P.theta + ffn_param_count(P.d, c->cfg.act_dim) : nullptr;
   if (c->cfg.model_kind == DDRL_MODEL_FFN) launch_forward_ffn(c->stream, fa);
   else launch_forward_gnn(c->stream, fa);
   HIPCHK(hipGetLastError());

@@ -157,6 +157,7 @@ struct NetLds {
   float* b2;
   float* wo;
   float* bo;
+  float* cup;   // update kernel, policy branch of the "cup" model: leg-coupling table [4][A]
 };
 
 // Per-lane LDS bases for the "R" pattern (row = 4s + q): rbase(v) = (4v + q)*64 + (c ^ swz),

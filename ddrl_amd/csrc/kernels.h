@@ -16,6 +16,7 @@
 struct RecLayout {
   int stride;      // floats per row (multiple of 4)
   int obs, act, logit, logp, vf, adv, vt, rew;
+  int cid;         // leg index of the row ("cup" model), -1 when the model has no coupling
 };
 
 // Per-policy routing tables for the observe / act / reward kernels.
@@ -62,6 +63,7 @@ struct ActArgs {
   const float* theta[DDRL_MAXP];
   const float* stage[DDRL_MAXP];   // [C][d] (ffn) or [N][4][23] (gnn)
   float* rec[DDRL_MAXP];           // base of the record buffer of this policy
+  const float* cup[DDRL_MAXP];     // "cup" leg-coupling table [4][A] (nullptr: none)
   float* last_v[DDRL_MAXP];
   RecLayout lay[DDRL_MAXP];
   int C[DDRL_MAXP];
@@ -115,6 +117,7 @@ struct UpdateArgs {
   float* grad_out;             // optional: write raw (unclipped) grads and stop (DDP)
   float* gscr;                 // [n_params] gradient scratch (L2 resident)
   float kl_coeff;
+  int cup;                     // "cup" model: the leg-coupling table follows the fcnet variables
 };
 struct UpdateHyper {
   float clip, vf_clip, vf_coeff, ent_coeff, lr, grad_clip, b1, b2, eps;
@@ -123,8 +126,9 @@ struct UpdateHyper {
 };
 // ua_dev: device array of h.P UpdateArgs (one persistent workgroup per entry)
 // ksp: 1 = one workgroup per branch, 2 = row split over two (gx: gx_bytes(P) of exchange granules)
+// d / stride: the widest obs width / record stride of the launched policies
 void launch_update_ffn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHyper& h, int nrows, float inv_n, int A, int d,
-                       unsigned long long* xchg, unsigned long long* gx, int ksp, int* err);
+                       int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp, int* err);
 size_t gx_bytes(int P);
 // clip_by_global_norm + tf1 Adam on a flat (all-reduced) gradient vector
 void launch_apply_adam(hipStream_t s, const float* grad, int n, float* theta, float* m, float* v,
@@ -133,6 +137,7 @@ void launch_apply_adam(hipStream_t s, const float* grad, int n, float* theta, fl
 // ---- ModelV2.forward / value_function on arbitrary rows ----
 struct ForwardArgs {
   const float* theta; const float* x; const int32_t* node; int n, d, A;
+  const float* cup;             // ffn: leg-coupling table [4][A] ("cup" model) or nullptr
   float* logits; float* values;
 };
 void launch_forward_ffn(hipStream_t s, const ForwardArgs& fa);

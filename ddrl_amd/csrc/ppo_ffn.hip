@@ -40,8 +40,11 @@ struct Geo {
 __host__ __device__ constexpr int waves_for(int A, int ksp) { return ksp == 2 ? 4 : (A == 8 ? 4 : 8); }
 // value pairs per lane of the partner exchange: small params + stats (padded to a pair),
 // then two per owned dW tile
+// coupling-table slots ("cup" model, models/coupling_net_glorot_uniform_init.py:11-30) among a
+// branch's small parameters: policy branch of the A = 2 kernels
+__host__ __device__ constexpr int ncup_slots(int OB, bool pol) { return pol && OB == 4 ? 2 * OB : 0; }
 __host__ __device__ constexpr int gx_pairs(int OB, int NW) {
-  return ((64 * OB + OB + 128 + 64 * NW - 1) / (64 * NW) + 2) / 2 + 2 * (16 / NW + (12 + NW - 1) / NW);
+  return ((64 * OB + OB + 128 + ncup_slots(OB, true) + 64 * NW - 1) / (64 * NW) + 2) / 2 + 2 * (16 / NW + (12 + NW - 1) / NW);
 }
 #define GX_MAX_PAIRS 20
 
@@ -62,9 +65,10 @@ __device__ __forceinline__ unsigned xchg_tag(unsigned epoch, int step) {
 }
 
 // Per-branch view of the flat (Keras-order) parameter vector.
-struct BranchOff { int w1, b1, w2, b2, wo, bo; };
+struct BranchOff { int w1, b1, w2, b2, wo, bo, cup; };
 __device__ __forceinline__ BranchOff branch_off(const FfnOffsets& o, bool pol) {
   BranchOff b;
+  b.cup = o.n;   // "cup" model: the leg-coupling table [4][A] follows the fcnet variables
   b.w1 = pol ? o.w1 : o.vw1; b.b1 = pol ? o.b1 : o.vb1;
   b.w2 = pol ? o.w2 : o.vw2; b.b2 = pol ? o.b2 : o.vb2;
   b.wo = pol ? o.wo : o.vo;  b.bo = pol ? o.bo : o.vbo;
@@ -73,9 +77,10 @@ __device__ __forceinline__ BranchOff branch_off(const FfnOffsets& o, bool pol) {
 
 template <int OB>
 __device__ void stage_branch(const float* __restrict__ th, int d, const BranchOff& bo, float* lds,
-                             NetLds& W) {
+                             NetLds& W, int ncup) {
   W.w1 = lds; W.w2 = W.w1 + 48 * 64; W.b1 = W.w2 + 64 * 64; W.b2 = W.b1 + 64;
-  W.wo = W.b2 + 64; W.bo = W.wo + 64 * OB;
+  W.wo = W.b2 + 64; W.bo = W.wo + 64 * OB; W.cup = W.bo + OB;   // cup: OB <= 4 (A = 2)
+  for (int i = threadIdx.x; i < ncup; i += blockDim.x) W.cup[i] = th[bo.cup + i];
   for (int i = threadIdx.x; i < 48 * 64; i += blockDim.x) {
     const int f = i >> 6;
     W.w1[sidx(f, i & 63)] = f < d ? th[bo.w1 + i] : 0.f;
@@ -87,7 +92,8 @@ __device__ void stage_branch(const float* __restrict__ th, int d, const BranchOf
 }
 #define BRANCH_LDS_FLOATS (48 * 64 + 64 * 64 + 128 + 64 * 16 + 16)   // multiple of 4 floats
 
-// "Small" parameters owned one per thread: [dWo 64*OB][dbo OB][db1 64][db2 64]
+// "Small" parameters owned one per thread: [dWo 64*OB][dbo OB][db1 64][db2 64], then the
+// policy branch's leg-coupling table [4][A] of the "cup" model
 template <int OB>
 __device__ __forceinline__ void small_param(int e, const BranchOff& bo, const NetLds& W, int& pidx, float*& lp) {
   if (e < 64 * OB) { pidx = bo.wo + e; lp = W.wo + e; return; }
@@ -96,8 +102,11 @@ __device__ __forceinline__ void small_param(int e, const BranchOff& bo, const Ne
   e -= OB;
   if (e < 64) { pidx = bo.b1 + e; lp = W.b1 + e; return; }
   e -= 64;
-  pidx = bo.b2 + e; lp = W.b2 + e;
+  if (e < 64) { pidx = bo.b2 + e; lp = W.b2 + e; return; }
+  e -= 64;
+  pidx = bo.cup + e; lp = W.cup + e;
 }
+
 
 template <int A, int RT>
 struct RowData {
@@ -105,6 +114,7 @@ struct RowData {
   float act[RT][A];
   float ol[RT][2 * A];
   float s0[RT], s1[RT];  // policy: logp_old, adv;  value: vf_old, vt
+  int cid[RT];           // "cup": coupling row of the record
 };
 
 // The next minibatch's 128 records are gathered by LDS-DMA into stg [128][stride] while the
@@ -155,7 +165,9 @@ __device__ __forceinline__ void load_row(const float* stg, int stg_stride, const
       for (int j = 0; j < 2 * A; ++j) r.ol[t][j] = rp[L.logit + j];
       r.s0[t] = rp[L.logp];
       r.s1[t] = rp[L.adv];
+      r.cid[t] = L.cid >= 0 ? min(max((int)rp[L.cid], 0), 3) : 0;
     } else {
+      r.cid[t] = 0;
 #pragma unroll
       for (int j = 0; j < A; ++j) r.act[t][j] = 0.f;
 #pragma unroll
@@ -304,7 +316,7 @@ __device__ __forceinline__ void gx_get(__amdgpu_buffer_rsrc_t r, unsigned tag, f
   }
 }
 
-template <int A, int KS1, int OB, bool POL, int NW, int KSP>
+template <int A, int KS1, int OB, bool POL, int NW, int KSP, bool CUP>
 __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBatch& ub, float* lds, int p, int kq) {
   constexpr int ROWS = DDRL_MB / KSP;
   constexpr int NT = Geo<NW, ROWS>::NT, RT = Geo<NW, ROWS>::RT, NS1 = Geo<NW, ROWS>::NS1, NS2 = Geo<NW, ROWS>::NS2;
@@ -313,7 +325,11 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   const FfnOffsets of = ffn_offsets(d, A);
   const BranchOff bo = branch_off(of, POL);
   const int nf1 = (d + 15) >> 4;
-  constexpr int NSB = 64 * OB + OB + 128;          // small params of this branch
+  constexpr int NSB0 = 64 * OB + OB + 128;         // small params of this branch
+  constexpr int NCUP = CUP ? ncup_slots(OB, POL) : 0;   // + the "cup" coupling table
+  constexpr int NSB = NSB0 + NCUP;                  // small params of this branch
+  constexpr bool cup = NCUP > 0;
+  constexpr int nsb = NSB;
   constexpr int NSLOT = (NSB + NT - 1) / NT;
   constexpr int NSTAT = POL ? 3 : 5;
   constexpr int NTS = NS1 + NS2;
@@ -322,7 +338,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   static_assert(KSP == 1 || (NT == 256 && NP == gx_pairs(OB, NW) && NP <= GX_MAX_PAIRS), "exchange pairs");
 
   NetLds W;
-  stage_branch<OB>(U.theta, d, bo, lds, W);
+  stage_branch<OB>(U.theta, d, bo, lds, W, NCUP);
   constexpr int LD = ROWS + 8;              // feature-major image stride
   float* bufA = lds + BRANCH_LDS_FLOATS;    // feature-major [64][LD]: H1, then X
   float* bufB = bufA + 64 * LD;             // feature-major [64][LD]: dZ2, then dZ1
@@ -368,7 +384,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   for (int k = 0; k < NSLOT; ++k) {
     const int e = tid + NT * k;
     ms[k] = vs[k] = 0.f;
-    if (e < NSB) {
+    if (e < nsb) {
       int pidx; float* lp;
       small_param<OB>(e, bo, W, pidx, lp);
       ms[k] = U.m[pidx];
@@ -409,6 +425,20 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     floatx4 h1[RT][4], h2[RT][4], dz[RT][4];
     float out[RT][OB], dout[RT][OB];
     ffn_fwd_rt<OB, KS1, RT>(W, cur.x, h1, h2, out);
+    // "cup" (coupling_net_glorot_uniform_init.py:22-30): means scaled by the record's leg row
+    float pre[RT][A], cf[RT][A];
+    if constexpr (cup) {
+      {
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+          for (int j = 0; j < A; ++j) {
+            pre[t][j] = out[t][j];
+            cf[t][j] = W.cup[cur.cid[t] * A + j];
+            out[t][j] *= cf[t][j];
+          }
+      }
+    }
     STAMP(0);
     float st[NSTAT];
 #pragma unroll
@@ -426,6 +456,26 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     }
     STAMP(1);
     float* Pw = Pb + w * NSB;
+    if constexpr (cup) {
+      {
+        // d coupling[leg][j] = sum over the leg's rows of dmean_j * pre-coupling mean_j;
+        // the fcnet head then sees dmean_j * coupling[leg][j]
+#pragma unroll
+        for (int lg = 0; lg < 4; ++lg)
+#pragma unroll
+          for (int j = 0; j < A; ++j) {
+            float v = 0.f;
+#pragma unroll
+            for (int t = 0; t < RT; ++t) v += cur.cid[t] == lg ? dout[t][j] * pre[t][j] : 0.f;
+            v = row16_sum(v);
+            if (lane == 0) Pw[NSB0 + lg * A + j] = v;
+          }
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+          for (int j = 0; j < A; ++j) dout[t][j] *= cf[t][j];
+      }
+    }
     // head weight / bias partial gradients over this wave's rows: DPP transpose-reduce
     // of the 16 features (fb, r) a lane holds; afterwards lane (c, q) owns feature
     // h = 16 (c >> 2) + 4 q + (c & 3).
@@ -516,7 +566,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       for (int k = 0; k < NSLOT; ++k) {
         const int e = tid + NT * k;
         float sm = 0.f;
-        if (e < NSB)
+        if (e < nsb)
           for (int i = 0; i < NW; ++i) sm += Pb[i * NSB + e];
         gs[k] = sm;
         v0[k] = sm;
@@ -609,7 +659,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       for (int k = 0; k < NSLOT; ++k) {
         const int e = tid + NT * k;
         float sm = 0.f;
-        if (e < NSB)
+        if (e < nsb)
           for (int i = 0; i < NW; ++i) sm += Pb[i * NSB + e];
         gs[k] = sm;
       }
@@ -636,7 +686,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 #pragma unroll
       for (int k = 0; k < NSLOT; ++k) {
         const int e = tid + NT * k;
-        if (e < NSB) {
+        if (e < nsb) {
           int pidx; float* lp;
           small_param<OB>(e, bo, W, pidx, lp);
           U.grad_out[pidx] = gs[k];
@@ -699,7 +749,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       for (int k = 0; k < NSLOT; ++k) {
         const int e = tid + NT * k;
         ts[k] = 0.f;
-        if (e < NSB) { int pidx; float* lp; small_param<OB>(e, bo, W, pidx, lp); ts[k] = *lp; }
+        if (e < nsb) { int pidx; float* lp; small_param<OB>(e, bo, W, pidx, lp); ts[k] = *lp; }
       }
 #pragma unroll
       for (int i = 0; i < NTS; ++i)
@@ -729,7 +779,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 #pragma unroll
       for (int k = 0; k < NSLOT; ++k) {
         const int e = tid + NT * k;
-        if (e < NSB) { int pidx; float* lp; small_param<OB>(e, bo, W, pidx, lp); *lp = ts[k]; }
+        if (e < nsb) { int pidx; float* lp; small_param<OB>(e, bo, W, pidx, lp); *lp = ts[k]; }
       }
     }
 #endif
@@ -759,7 +809,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 #pragma unroll
   for (int k = 0; k < NSLOT; ++k) {
     const int e = tid + NT * k;
-    if (e >= NSB) continue;
+    if (e >= nsb) continue;
     int pidx; float* lp;
     small_param<OB>(e, bo, W, pidx, lp);
     U.m[pidx] = ms[k];
@@ -777,7 +827,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   }
 }
 
-template <int A, int KS1, int KSP>
+template <int A, int KS1, int KSP, bool CUP>
 __global__ void __launch_bounds__(64 * waves_for(A, KSP)) k_update_ffn(UpdateBatch ub) {
   extern __shared__ float lds[];
   constexpr int NW = waves_for(A, KSP);
@@ -788,30 +838,31 @@ __global__ void __launch_bounds__(64 * waves_for(A, KSP)) k_update_ffn(UpdateBat
   if (p >= ub.h.P) return;
   const int j = blockIdx.x >> 3, branch = j / KSP, kq = j - branch * KSP;
   const UpdateArgs U = ub.a[p];
-  if (branch) update_loop<A, KS1, 1, false, NW, KSP>(U, ub, lds, p, kq);
-  else update_loop<A, KS1, 2 * A, true, NW, KSP>(U, ub, lds, p, kq);
+  if (branch) update_loop<A, KS1, 1, false, NW, KSP, false>(U, ub, lds, p, kq);
+  else update_loop<A, KS1, 2 * A, true, NW, KSP, CUP>(U, ub, lds, p, kq);
 }
 
 // stride: the widest record stride of the launched policies (staging buffer rows)
 static size_t update_lds_bytes(int O, int stride, int ksp) {
-  const int nsb = 64 * O + O + 128;
+  const int nsb = 64 * O + O + 128 + ncup_slots(O, true);
   const int nw = waves_for(O / 2, ksp);
   return (size_t)(BRANCH_LDS_FLOATS + 2 * 64 * (DDRL_MB / ksp + 8) + nw * nsb + 256 +
                   (DDRL_MB / ksp) * 4 * stg_chunks(stride, O / 2)) * 4;
 }
 
-template <int A, int KS1>
+template <int A, int KS1, bool CUP = false>
 static void launch_update_t(hipStream_t s, const UpdateBatch& ub, int P, int stride, int ksp) {
   if (ksp == 2)
-    hipLaunchKernelGGL((k_update_ffn<A, KS1, 2>), dim3(24 + P), dim3(64 * waves_for(A, 2)),
+    hipLaunchKernelGGL((k_update_ffn<A, KS1, 2, CUP>), dim3(24 + P), dim3(64 * waves_for(A, 2)),
                        update_lds_bytes(2 * A, stride, 2), s, ub);
   else
-    hipLaunchKernelGGL((k_update_ffn<A, KS1, 1>), dim3(8 + P), dim3(64 * waves_for(A, 1)),
+    hipLaunchKernelGGL((k_update_ffn<A, KS1, 1, CUP>), dim3(8 + P), dim3(64 * waves_for(A, 1)),
                        update_lds_bytes(2 * A, stride, 1), s, ub);
 }
 
 void launch_update_ffn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHyper& h, int nrows, float inv_n,
-                       int A, int d, unsigned long long* xchg, unsigned long long* gx, int ksp, int* err) {
+                       int A, int d, int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp,
+                       int* err) {
   UpdateBatch ub;
   ub.a = ua_dev;
   ub.h = h;
@@ -825,8 +876,10 @@ void launch_update_ffn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHype
   // clear the previous launch's granules (the epoch in every tag keeps them apart anyway)
   (void)hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * 4 * ksp * h.P, s);
   if (ksp == 2) (void)hipMemsetAsync(gx, 0, gx_bytes(h.P), s);
-  const int stride = (d + 3 * A + 5 + 3) & ~3;   // RecLayout stride of the widest policy (capi make_layout)
-  DDRL_DISPATCH_A_KS1(A, d, launch_update_t, s, ub, h.P, stride, ksp);
+  if (cup)   // "cup": one shared leg policy, A = 2, d <= 20 (capi validate)
+    launch_update_t<2, 5, true>(s, ub, h.P, stride, ksp);
+  else
+    DDRL_DISPATCH_A_KS1(A, d, launch_update_t, s, ub, h.P, stride, ksp);
 }
 
 size_t gx_bytes(int P) { return sizeof(unsigned long long) * (size_t)P * 2 * 2 * 2 * GX_MAX_PAIRS * 256 * 2; }

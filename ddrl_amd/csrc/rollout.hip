@@ -275,6 +275,12 @@ __global__ void __launch_bounds__(256) k_act_ffn(RouteArgs ra, ActArgs aa) {
   float* rp = aa.rec[p] + ((size_t)aa.t * C + row) * L.stride;
   const int e = row / pr.k, slot = row - e * pr.k;
   const int agent = pr.agent[slot];
+  // "cup" model (coupling_net_glorot_uniform_init.py:22-30): mean_j *= coupling[leg][j], the
+  // log-std half is padded with ones; leg = the agent's index in the env (one shared policy)
+  if (aa.cup[p]) {
+#pragma unroll
+    for (int j = 0; j < A; ++j) logits[j] *= aa.cup[p][slot * A + j];
+  }
   // sample + logp (DiagGaussian, RLlib 1.0): a = mean + std * eps
   float logp = -0.5f * (float)(DDRL_LOG2PI * A);
   float act[A];
@@ -303,6 +309,7 @@ __global__ void __launch_bounds__(256) k_act_ffn(RouteArgs ra, ActArgs aa) {
   } else if (q == 2) {
     rp[L.logp] = logp;
     rp[L.vf] = vout[0];
+    if (L.cid >= 0) rp[L.cid] = (float)slot;
   }
 }
 
@@ -403,6 +410,11 @@ __global__ void __launch_bounds__(256) k_forward_ffn(ForwardArgs fa) {
   ffn_branch_fwd<1, KS1>(VW, xop, h1, h2, vout);
   ffn_branch_fwd<O, KS1>(PW, xop, h1, h2, logits);
   if (!valid) return;
+  if (fa.cup) {   // "cup": leg index of the row (clamped to the table; the host validates it)
+    const int leg = min(max(fa.node[row], 0), 3);
+#pragma unroll
+    for (int j = 0; j < A; ++j) logits[j] *= fa.cup[leg * A + j];
+  }
   if (q == 0) fa.values[row] = vout[0];
   for (int j = q; j < O; j += 4) fa.logits[(size_t)row * O + j] = logits[j];
 }

@@ -1,7 +1,8 @@
 """Mirror of the reference's model registry (models/__init__.py:7-13) over the HIP path.
 
 ModelCatalog names: "ffn" and "fc_glorot_uniform_init" -> fcnet with Glorot-uniform init
-(models/fcnet_glorot_uniform_init.py:10-125); "gnn" -> GraphNet actor/critic
+(models/fcnet_glorot_uniform_init.py:10-125); "cup" -> fcnet + trainable leg coupling
+(models/coupling_net_glorot_uniform_init.py:11-137); "gnn" -> GraphNet actor/critic
 (models/shared_graphnet_glorot_uniform_init.py:14-58).  A model instance exposes the
 ModelV2 surface the reference's plugins implement: forward(input_dict, state, seq_lens)
 -> (logits, state) and value_function() -> [B]; the arithmetic runs in libddrl_hip.so.
@@ -98,6 +99,28 @@ class FullyConnectedNetwork_GNN_GlorotUniformInitializer(_HipModel):
         return logits, state
 
 
+class FullyConnectedNetwork_Coupling_GlorotUniformInitializer(_HipModel):
+    """"cup" (models/coupling_net_glorot_uniform_init.py:32-137): the fcnet on the features
+    of the (leg index, features) observation, whose action means are scaled by the trainable
+    leg_coupling row of the leg index (LegCoupling, :11-30)."""
+
+    def forward(self, input_dict, state, seq_lens):
+        import torch
+        self._need_ctx()
+        leg, x = input_dict["obs"]
+        x = torch.as_tensor(x, dtype=torch.float32, device="cuda").contiguous()
+        leg = torch.as_tensor(leg, device="cuda").reshape(-1).to(torch.int32).contiguous()
+        if leg.numel() and (int(leg.min()) < 0 or int(leg.max()) > 3):
+            raise ValueError("leg index out of range [0, 3]")
+        n = x.shape[0]
+        logits = torch.empty((n, self.num_outputs), dtype=torch.float32, device="cuda")
+        values = torch.empty((n,), dtype=torch.float32, device="cuda")
+        self.ctx.policy_forward(self.pid, x, n, logits, values, node_dev=leg)
+        self._value_out = values
+        return logits, state
+
+
 ModelCatalog.register_custom_model("ffn", FullyConnectedNetwork_GlorotUniformInitializer)
+ModelCatalog.register_custom_model("cup", FullyConnectedNetwork_Coupling_GlorotUniformInitializer)
 ModelCatalog.register_custom_model("gnn", FullyConnectedNetwork_GNN_GlorotUniformInitializer)
 ModelCatalog.register_custom_model("fc_glorot_uniform_init", FullyConnectedNetwork_GlorotUniformInitializer)

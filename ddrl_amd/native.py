@@ -39,6 +39,7 @@ class DdrlCfg(C.Structure):
         ("adam_beta1", f32), ("adam_beta2", f32), ("adam_eps", f32),
         ("vf_clip_mode", i32), ("sgd_minibatch_size", i32), ("num_sgd_iter", i32),
         ("act_negate", (i32 * 8) * MAX_AG), ("policy_filter", i32),
+        ("leg_coupling", i32),
     ]
 
 
@@ -98,6 +99,9 @@ def header_symbols(path=HEADER):
     return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(ddrl_\w+)\s*\(", txt, re.M)))
 
 
+ABI_VERSION = 3   # DDRL_ABI_VERSION of include/ddrl_hip.h (ddrl_cfg layout, record layout)
+
+
 def load(path: str = LIB_PATH):
     global _lib
     if _lib is not None:
@@ -113,6 +117,9 @@ def load(path: str = LIB_PATH):
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
+    if lib.ddrl_abi_version() != ABI_VERSION:
+        raise DdrlError(f"{path} has ABI {lib.ddrl_abi_version()}, this binding expects {ABI_VERSION}: "
+                        "rebuild with `python -m ddrl_amd.build`")
     _lib = lib
     return lib
 
@@ -155,10 +162,10 @@ class Context:
             n = C.c_int64()
             _ck(self.lib.ddrl_param_count(h, p, C.byref(n)))
             self.n_params.append(int(n.value))
-            lay = (i32 * 10)()
+            lay = (i32 * 11)()
             _ck(self.lib.ddrl_record_layout(h, p, lay))
             self.layout.append(dict(zip(
-                ["stride", "obs", "act", "logit", "logp", "vf", "adv", "vt", "rew", "C"], list(lay))))
+                ["stride", "obs", "act", "logit", "logp", "vf", "adv", "vt", "rew", "C", "leg"], list(lay))))
 
     def close(self):
         if getattr(self, "h", None):

@@ -184,6 +184,7 @@ class QuantrupedSingleDecentralizedLegIDEnv(QuantrupedSingleControllerSuperEnv):
     (d = 23): `policy_obs_indices` encodes the one-hot as the constants -1 (0.0) and -2
     (1.0) of the gather table."""
     leg_angles = {'agent_FL': 45., 'agent_HL': 135., 'agent_HR': -135., 'agent_FR': -45.}
+    leg_index_obs = True   # (leg index, features): the "cup" model consumes the tuple as is
 
     def _init_tables(self):
         super()._init_tables()

@@ -33,6 +33,14 @@ def make_cfg(env, n_envs, frag_len=None, config=None):
     if isinstance(env, str):
         env = get_env_class(env)
     inst = env(env_config) if isinstance(env, type) else env
+    custom_model = (config.get("model") or {}).get("custom_model")
+    # "cup" (models/coupling_net_glorot_uniform_init.py:32-137) takes the LegID env's
+    # (leg index, features) tuple: the features are the model input and the index selects
+    # the coupling row, so the model reads obs_indices (no one-hot columns)
+    cup = custom_model == "cup"
+    if cup and not getattr(inst, "leg_index_obs", False):
+        raise ValueError(f"custom_model 'cup' needs an env whose observation is (leg index, features) "
+                         f"(QuantrupedMultiEnv_SharedDecentralLegID); got {type(inst).__name__}")
     if inst.model_kind not in ("ffn", "gnn"):
         raise ValueError(f"{type(inst).__name__}: no model of the reference fits this env's observations "
                          "(SURVEY Appendix B.8)")
@@ -50,7 +58,7 @@ def make_cfg(env, n_envs, frag_len=None, config=None):
     for j, a in enumerate(agents):
         p = policies.index(mapping(a))
         c.agent_policy[j] = p
-        idx = getattr(inst, "policy_obs_indices", inst.obs_indices)[a]   # model input columns
+        idx = (inst.obs_indices if cup else getattr(inst, "policy_obs_indices", inst.obs_indices))[a]
         c.obs_dim[p] = len(idx)
         for f, i in enumerate(idx):
             c.obs_index[j][f] = i
@@ -87,4 +95,5 @@ def make_cfg(env, n_envs, frag_len=None, config=None):
     if config["observation_filter"] not in ("NoFilter", "MeanStdFilter"):
         raise ValueError(f"observation_filter {config['observation_filter']!r} is not supported")
     c.policy_filter = 1 if config["observation_filter"] == "MeanStdFilter" else 0
+    c.leg_coupling = 1 if cup else 0
     return c, inst

@@ -35,6 +35,12 @@ def glorot_ffn_flat(rng, d, A, hidden=64):
     return np.concatenate([p.reshape(-1) for p in parts])
 
 
+def leg_coupling_init(A):
+    """LegCoupling.build (models/coupling_net_glorot_uniform_init.py:20): the table starts at
+    [[1, 1], [-1, -1], [-1, -1], [1, 1]] (FL, HL, HR, FR), not at a random draw."""
+    return np.resize(np.array([[1, 1], [-1, -1], [-1, -1], [1, 1]], np.float32), (4, A)).reshape(-1)
+
+
 class PPOTrainer:
     """Multi-agent PPO on one device (one env shard).
 
@@ -69,7 +75,10 @@ class PPOTrainer:
         self.sched_rng = np.random.default_rng(seed + 7919 * (self.rank + 1))
         for p in range(P):
             if self.cfg.model_kind == N.MODEL_FFN:
-                self.ctx.params_set(p, glorot_ffn_flat(self.rng, self.cfg.obs_dim[p], self.cfg.act_dim))
+                theta = glorot_ffn_flat(self.rng, self.cfg.obs_dim[p], self.cfg.act_dim)
+                if self.cfg.leg_coupling:
+                    theta = np.concatenate([theta, leg_coupling_init(self.cfg.act_dim)])
+                self.ctx.params_set(p, theta)
             else:
                 from .models import glorot_gnn_flat
                 self.ctx.params_set(p, glorot_gnn_flat(self.rng, self.cfg.act_dim))

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define DDRL_ABI_VERSION 2
+#define DDRL_ABI_VERSION 3
 #define DDRL_MAX_POLICIES 4
 #define DDRL_MAX_AGENTS 4
 #define DDRL_MAX_OBS 48
@@ -75,6 +75,11 @@ typedef struct ddrl_cfg {
                                               vector (LegTransforms: fr / hr knee)          */
   int32_t policy_filter;    /* RLlib observation_filter "MeanStdFilter" on every policy's
                                input (after the env-side filter; unclipped, fp64 stats)     */
+  int32_t leg_coupling;     /* "cup" model (models/coupling_net_glorot_uniform_init.py:11-30,
+                               registered models/__init__.py:10): the action means of the
+                               shared leg policy are scaled by a trainable table [4][A],
+                               row = the agent's leg index (SharedDecentralLegID env, :66-114);
+                               the table follows the fcnet variables in the parameter vector */
 } ddrl_cfg;
 
 typedef struct ddrl_ctx ddrl_ctx;
@@ -88,8 +93,9 @@ int ddrl_ctx_destroy(ddrl_ctx* ctx);
 int ddrl_set_stream(ddrl_ctx* ctx, void* hip_stream);
 int ddrl_synchronize(ddrl_ctx* ctx);
 
-/* Shapes.  layout_out[10] = {row_stride, off_obs, off_act, off_logits, off_logp, off_vf,
- * off_adv, off_vt, off_rew, rows_per_step (C = N*k)}, all in floats. */
+/* Shapes.  layout_out[11] = {row_stride, off_obs, off_act, off_logits, off_logp, off_vf,
+ * off_adv, off_vt, off_rew, rows_per_step (C = N*k), off_leg (leg index of the row, "cup"
+ * model; -1 otherwise)}, all in floats. */
 int ddrl_param_count(ddrl_ctx* ctx, int pid, int64_t* n_out);
 int ddrl_record_layout(ddrl_ctx* ctx, int pid, int32_t* layout_out);
 
@@ -163,7 +169,8 @@ int ddrl_ppo_grad(ddrl_ctx* ctx, int pid, const int32_t* rows_dev, int n_rows,
 int ddrl_ppo_apply(ddrl_ctx* ctx, int pid, const float* grad_dev);
 
 /* Model forward (ModelV2.forward + value_function) on arbitrary rows:
- * obs_dev[n][d] (ffn) or X_dev[n][4][23] + node_dev[n] (gnn). */
+ * obs_dev[n][d] (ffn; + node_dev[n] = leg index with leg_coupling) or X_dev[n][4][23] +
+ * node_dev[n] (gnn). */
 int ddrl_policy_forward(ddrl_ctx* ctx, int pid, const float* obs_dev, const int32_t* node_dev,
                         int n, float* logits_dev, float* values_dev);
 

@@ -250,6 +250,44 @@ def ffn_backward(p, cache, dlogits, dvalue):
 
 
 # --------------------------------------------------------------------------------------
+# f4  "cup": fcnet + trainable leg coupling (models/coupling_net_glorot_uniform_init.py:11-30,
+#     model :32-137; registered models/__init__.py:10).  LegCoupling.build starts the table
+#     at [[1,1],[-1,-1],[-1,-1],[1,1]] (:20); call() pads it with ones for the log-std half
+#     (:27) and gathers the row of the agent's leg index (:28), so only the means are scaled.
+#     The variable follows the fcnet variables (register_variables order, :136-137).
+# --------------------------------------------------------------------------------------
+LEG_COUPLING_INIT = np.array([[1, 1], [-1, -1], [-1, -1], [1, 1]], F32)
+
+
+def cup_param_shapes(d, A, hidden=64):
+    return ffn_param_shapes(d, 2 * A, hidden) + [("leg_coupling", (4, A))]
+
+
+def cup_init(rng, d, A, hidden=64):
+    p = ffn_init(rng, d, 2 * A, hidden)
+    p["leg_coupling"] = np.resize(LEG_COUPLING_INIT, (4, A)).astype(F32)
+    return p
+
+
+def cup_forward(p, x, leg):
+    logits, value, cache = ffn_forward(p, x)
+    leg = np.asarray(leg).reshape(-1).astype(np.int64)
+    A = p["leg_coupling"].shape[1]
+    coef = np.concatenate([p["leg_coupling"], np.ones_like(p["leg_coupling"])], 1)[leg]
+    return (logits * coef).astype(F32), value, (cache, logits, leg, coef, A)
+
+
+def cup_backward(p, cache, dlogits, dvalue):
+    fcache, pre, leg, coef, A = cache
+    dlogits = np.asarray(dlogits, F32)
+    g = ffn_backward(p, fcache, dlogits * coef, dvalue)
+    gc = np.zeros((4, A), F32)
+    np.add.at(gc, leg, (dlogits * pre)[:, :A])
+    g["leg_coupling"] = gc
+    return g
+
+
+# --------------------------------------------------------------------------------------
 # a9 / a10  GraphNet + MPNN (models/graph_net.py:8-45, models/gcn.py:39-94,
 #           models/shared_graphnet_glorot_uniform_init.py:14-58)
 # --------------------------------------------------------------------------------------
@@ -529,8 +567,8 @@ def update_kl(kl_coeff, sampled_kl, kl_target=0.01):
 
 
 def ppo_update(model, params, shapes, adam, batch, shuffle, perms, kl_coeff, cfg, steps=None):
-    """Runs the minibatch loop for one policy.  `model` is "ffn" or "gnn".  `batch` is a
-    dict of row arrays: obs (or X/node_idx), actions, logits, logp, vf_preds, adv
+    """Runs the minibatch loop for one policy.  `model` is "ffn", "cup" or "gnn".  `batch` is
+    a dict of row arrays: obs (+ leg for "cup"; X/node_idx for "gnn"), actions, logits, logp, vf_preds, adv
     (already standardized) and vt.  Returns (params, per-step stats list)."""
     mb = cfg.get("sgd_minibatch_size", 128)
     epochs, nb = perms.shape
@@ -545,6 +583,8 @@ def ppo_update(model, params, shapes, adam, batch, shuffle, perms, kl_coeff, cfg
             p = unpack(theta, shapes)
             if model == "ffn":
                 logits, value, cache = ffn_forward(p, batch["obs"][rows])
+            elif model == "cup":
+                logits, value, cache = cup_forward(p, batch["obs"][rows], batch["leg"][rows])
             else:
                 logits, value, cache = gnn_forward(p, batch["X"][rows], batch["node_idx"][rows])
             dlogits, dvalue, st = ppo_loss_rows(
@@ -553,7 +593,7 @@ def ppo_update(model, params, shapes, adam, batch, shuffle, perms, kl_coeff, cfg
                 batch["vt"][rows], np.float32(kl_coeff), cfg.get("clip_param", 0.2),
                 cfg.get("vf_clip_param", 10.0), cfg.get("vf_loss_coeff", 0.5),
                 cfg.get("entropy_coeff", 0.0))
-            g = (ffn_backward if model == "ffn" else gnn_backward)(p, cache, dlogits, dvalue)
+            g = {"ffn": ffn_backward, "cup": cup_backward, "gnn": gnn_backward}[model](p, cache, dlogits, dvalue)
             glist = [g[n] for n, _ in shapes]
             clipped, gn = clip_by_global_norm(glist, cfg.get("grad_clip", 0.5))
             flat = np.concatenate([c.reshape(-1) for c in clipped])

@@ -69,7 +69,7 @@ class OracleRollout:
     def observe(self, obs):
         normed = O.mean_std_filter(obs, self.rs, update=True, clip=self.cfg.filter_clip)
         self.stage = []
-        tables = getattr(self.inst, "policy_obs_indices", self.inst.obs_indices)
+        tables = self.model_tables()
         # gather columns; the constants -1 / -2 (LegID one-hot) become 0 / 1
         ext = np.concatenate([normed, np.zeros((normed.shape[0], 1)), np.ones((normed.shape[0], 1))], 1)
         col = lambda i: i if i >= 0 else normed.shape[1] + (-1 - i)
@@ -80,13 +80,19 @@ class OracleRollout:
                 x = O.mean_std_filter(x, self.pf[p], update=True, clip=None)
             self.stage.append(x.astype(np.float32))
 
+    def model_tables(self):
+        return getattr(self.inst, "policy_obs_indices", self.inst.obs_indices)
+
+    def forward(self, p, x):
+        return O.ffn_forward(self.params[p], x)
+
     def act(self, t, eps):
         cfg = self.cfg
         A = cfg.act_dim
         actions = np.zeros((cfg.n_envs, 8), np.float32)
         for p in range(cfg.n_policies):
             x = self.stage[p]
-            logits, value, _ = O.ffn_forward(self.params[p], x)
+            logits, value, _ = self.forward(p, x)
             k = len(self.slots[p])
             e_idx = [self.agents.index(a) for a in self.slots[p]]
             ep = eps[:, e_idx, :].reshape(-1, A)
@@ -119,7 +125,7 @@ class OracleRollout:
         self.done[t] = done
 
     def bootstrap(self):
-        self.last_v = [O.ffn_forward(self.params[p], self.stage[p])[1] for p in range(self.cfg.n_policies)]
+        self.last_v = [self.forward(p, self.stage[p])[1] for p in range(self.cfg.n_policies)]
 
     def gae(self):
         out = []
@@ -145,6 +151,8 @@ class OracleRollout:
         for key, off in (("logp", "logp"), ("vf", "vf"), ("rew", "rew"), ("adv", "adv"), ("vt", "vt")):
             if key in r:
                 out[:, lay[off]] = r[key].reshape(-1)
+        if lay.get("leg", -1) >= 0:   # "cup": leg index of the row = slot (c = e * k + slot)
+            out[:, lay["leg"]] = np.tile(np.arange(C) % len(self.slots[p]), T)
         return out
 
 
@@ -189,6 +197,37 @@ def run_rollout(ctx, cfg, inst, params, rng, filt, T, orc_cls=None):
     norms = orc.gae()
     torch.cuda.synchronize()
     return orc, norms, np.stack(acts_gpu), np.stack(acts_orc)
+
+
+# --------------------------------------------------------------------------------------
+# "cup" (SharedDecentralLegID env + leg-coupling fcnet): one shared leg policy, 4 rows per
+# env, leg index = slot; the model input is the 19 features (no one-hot columns).
+# --------------------------------------------------------------------------------------
+CUP_ENV = "QuantrupedMultiEnv_SharedDecentralLegID"
+CUP_CONFIG = {"model": {"custom_model": "cup"}}
+
+
+def init_cup_params(ctx, cfg, seed, head_scale=30.0, perturb=True):
+    rng = np.random.default_rng(seed)
+    A, d = cfg.act_dim, cfg.obs_dim[0]
+    pr = O.cup_init(rng, d, A)
+    pr["fc_out/kernel"] *= head_scale
+    pr["value_out/kernel"] *= head_scale
+    pr["fc_1/bias"] += rng.normal(size=64).astype(np.float32) * 0.1
+    pr["fc_out/bias"] += np.concatenate([np.zeros(A), -0.5 * np.ones(A)]).astype(np.float32)
+    if perturb:   # off the +-1 start so that every coupling entry scales differently
+        pr["leg_coupling"] = (pr["leg_coupling"] * rng.uniform(0.5, 1.5, size=(4, A))).astype(np.float32)
+    ctx.params_set(0, O.pack(pr, O.cup_param_shapes(d, A)))
+    return [pr]
+
+
+class CupOracleRollout(OracleRollout):
+    def model_tables(self):
+        return self.inst.obs_indices
+
+    def forward(self, p, x):
+        leg = np.arange(x.shape[0]) % len(self.slots[p])
+        return O.cup_forward(self.params[p], x, leg)
 
 
 # --------------------------------------------------------------------------------------

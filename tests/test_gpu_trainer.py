@@ -42,13 +42,15 @@ def pg1():
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("env,n", [("QuantrupedMultiEnv_Local", 64),
-                                   ("QuantrupedMultiEnv_SharedDecentral", 48),
-                                   ("QuantrupedMultiEnv_DecentralShared_Graph", 24),
-                                   ("QuantrupedMultiEnv_Centralized", 32)])
-def test_trainer_iteration(env, n):
+@pytest.mark.parametrize("env,n,model", [("QuantrupedMultiEnv_Local", 64, None),
+                                         ("QuantrupedMultiEnv_SharedDecentral", 48, None),
+                                         ("QuantrupedMultiEnv_DecentralShared_Graph", 24, None),
+                                         ("QuantrupedMultiEnv_Centralized", 32, None),
+                                         ("QuantrupedMultiEnv_SharedDecentralLegID", 32, "cup")])
+def test_trainer_iteration(env, n, model):
     from ddrl_amd.trainer import PPOTrainer
-    tr = PPOTrainer({"env": env, "rollout_fragment_length": 8}, n_envs=n, seed=3)
+    extra = {"model": {"custom_model": model}} if model else {}
+    tr = PPOTrainer({"env": env, "rollout_fragment_length": 8, **extra}, n_envs=n, seed=3)
     w0 = {k: v.copy() for k, v in tr.get_weights().items()}
     r = tr.train()
     assert r["timesteps_total"] == 8 * n

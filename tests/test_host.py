@@ -83,3 +83,19 @@ def test_trainer_config_keys_and_update_kl():
     assert update_kl(0.2, 0.01) == 0.2
     cfg, _ = make_cfg("QuantrupedMultiEnv_Local", 4, 2, {"lr": 1e-4, "num_sgd_iter": 3})
     assert cfg.lr == pytest.approx(1e-4) and cfg.num_sgd_iter == 3 and cfg.sgd_minibatch_size == 128
+
+
+def test_cup_model_reads_leg_features_and_sets_coupling():
+    """"cup" (models/coupling_net_glorot_uniform_init.py:32-137) on the LegID env: the model
+    input is the 19 features of the (leg index, features) tuple, the leg index selects the
+    coupling row; on an env without that tuple the reference model cannot be built."""
+    from ddrl_amd.models import ModelCatalog
+    from ddrl_amd.trainer import leg_coupling_init
+    cfg, inst = make_cfg("QuantrupedMultiEnv_SharedDecentralLegID", 4, 2, {"model": {"custom_model": "cup"}})
+    assert cfg.leg_coupling == 1 and cfg.obs_dim[0] == 19 and cfg.n_policies == 1
+    for j, a in enumerate(inst.agent_names):
+        assert list(cfg.obs_index[j][:19]) == list(inst.obs_indices[a])
+    np.testing.assert_array_equal(leg_coupling_init(2).reshape(4, 2), [[1, 1], [-1, -1], [-1, -1], [1, 1]])
+    assert ModelCatalog.get("cup").__name__ == "FullyConnectedNetwork_Coupling_GlorotUniformInitializer"
+    with pytest.raises(ValueError):
+        make_cfg("QuantrupedMultiEnv_SharedDecentral", 4, 2, {"model": {"custom_model": "cup"}})

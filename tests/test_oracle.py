@@ -150,6 +150,40 @@ def test_ffn_ppo_gradients_match_autograd(d):
         np.testing.assert_allclose(g[k], ref, rtol=1e-4, atol=2e-5 * np.abs(ref).max(), err_msg=k)
 
 
+def test_cup_gradients_match_autograd():
+    """"cup" (models/coupling_net_glorot_uniform_init.py:22-30): coupled means, including
+    the gradient of the trainable leg-coupling table, against torch autograd."""
+    rng = np.random.default_rng(7)
+    d, A, n = 19, 2, 128
+    p = O.cup_init(rng, d, A)
+    np.testing.assert_array_equal(p["leg_coupling"], [[1, 1], [-1, -1], [-1, -1], [1, 1]])
+    p["leg_coupling"] = p["leg_coupling"] * rng.uniform(0.5, 1.5, size=(4, A)).astype(np.float32)
+    p["fc_out/kernel"] *= 30
+    p["value_out/kernel"] *= 30
+    b = _rand_batch(rng, n, d, A)
+    leg = rng.integers(0, 4, size=n)
+    beta = 0.3
+    logits, value, cache = O.cup_forward(p, b["obs"], leg)
+    dl, dv, st = O.ppo_loss_rows(logits, value, b["actions"], b["logits"], b["logp"],
+                                 b["vf_preds"], b["adv"], b["vt"], np.float32(beta))
+    g = O.cup_backward(p, cache, dl, dv)
+    t = {k: torch.tensor(v, dtype=torch.float64, requires_grad=True) for k, v in p.items()}
+    x = torch.tensor(b["obs"], dtype=torch.float64)
+    h2 = torch.tanh(torch.tanh(x @ t["fc_1/kernel"] + t["fc_1/bias"]) @ t["fc_2/kernel"] + t["fc_2/bias"])
+    raw = h2 @ t["fc_out/kernel"] + t["fc_out/bias"]
+    coef = torch.cat([t["leg_coupling"], torch.ones(4, A, dtype=torch.float64)], 1)[torch.tensor(leg)]
+    g2 = torch.tanh(torch.tanh(x @ t["fc_value_1/kernel"] + t["fc_value_1/bias"]) @ t["fc_value_2/kernel"]
+                    + t["fc_value_2/bias"])
+    v = (g2 @ t["value_out/kernel"] + t["value_out/bias"])[:, 0]
+    loss = _torch_ppo_loss(raw * coef, v, b, beta, {})
+    loss.backward()
+    assert abs(loss.item() - st["total_loss"]) < 1e-5 * max(1, abs(loss.item()))
+    assert np.abs(g["leg_coupling"]).max() > 0
+    for k in p:
+        ref = t[k].grad.numpy()
+        np.testing.assert_allclose(g[k], ref, rtol=1e-4, atol=2e-5 * np.abs(ref).max(), err_msg=k)
+
+
 def test_gnn_gradients_match_autograd():
     rng = np.random.default_rng(5)
     p = O.gnn_init(rng, 4)
