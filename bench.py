@@ -137,6 +137,7 @@ def main():
     ap.add_argument("--env", default="QuantrupedMultiEnv_Local")
     ap.add_argument("--frag", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) iteration")
     ap.add_argument("--cpu-envs", type=int, default=512)
     ap.add_argument("--ddp-mode", default="local", choices=["split", "local"],
                     help="shared-policy envs on N>1 GPUs: per-rank rows per SGD step (see ddrl_amd/ddp.py)")
@@ -196,12 +197,38 @@ def main():
 
     ctx.observe(syn.obs[0])
 
-    def iteration(record):
-        done = syn.dones_for_fragment()
+    host = None
+
+    def rollout_host_io(done):
+        """The rollout through pinned host buffers (ddrl_act_host / ddrl_env_step_host), the
+        interface of a host-side env plane: every env step waits for its actions on the host
+        (the envs step there) before the env's answer goes back (PCIe both ways each step).
+        The envs' data cycles through a 4-slot pinned ring (contents do not matter here)."""
+        nonlocal host
+        if host is None:
+            pin = lambda x: x[:4].cpu().contiguous().pin_memory()
+            host = dict(obs=pin(syn.obs), eps=pin(syn.eps), fw=pin(syn.fw), cfrc=pin(syn.cfrc),
+                        act=torch.zeros((n_local, 8), dtype=torch.float32).pin_memory(),
+                        done=torch.zeros((4, n_local), dtype=torch.uint8).pin_memory())
+        host["done"].copy_(done[:4].cpu())
         for t in range(T):
-            ctx.act(t, syn.eps[t], syn.actions)
-            ctx.reward(t, syn.fw[t], syn.cfrc[t], syn.actions, done[t])
-            ctx.observe(syn.obs[t + 1])
+            s = t % 4
+            if t == 0:
+                ctx.step_host(0, host["obs"][0], host["eps"][0], host["act"])
+            else:
+                ctx.act_host(t, host["eps"][s], host["act"])
+            stream.synchronize()
+            ctx.env_step_host(t, host["fw"][s], host["cfrc"][s], host["done"][s], host["obs"][(t + 1) % 4])
+
+    def iteration(record, host_io=False):
+        done = syn.dones_for_fragment()
+        if host_io:
+            rollout_host_io(done)
+        else:
+            for t in range(T):
+                ctx.act(t, syn.eps[t], syn.actions)
+                ctx.reward(t, syn.fw[t], syn.cfrc[t], syn.actions, done[t])
+                ctx.observe(syn.obs[t + 1])
         ctx.bootstrap()
         ctx.gae()
         if ddp:
@@ -260,6 +287,27 @@ def main():
         es = torch.tensor([env_steps], device="cuda", dtype=torch.float64)
         dist.all_reduce(es)
         env_steps = int(es.item())
+
+    pcie = None
+    if world == 1 and not args.no_pcie and not ddp:
+        # one more iteration with the rollout through pinned host buffers (not part of value)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        iteration(False, host_io=True)
+        torch.cuda.synchronize()
+        it_s = time.perf_counter() - t1
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        rollout_host_io(syn.dones_for_fragment())
+        torch.cuda.synchronize()
+        ro_s = time.perf_counter() - t2
+        per_step_bytes = 4 * n_local * (cfg.obs_full_dim + cfg.n_agents * A + 8 + 1 + 14 * 6) + n_local
+        pcie = {"value": T * n_local / it_s, "unit": "env-steps/s", "iteration_ms": it_s * 1e3,
+                "rollout_ms": ro_s * 1e3, "rollout_env_steps_per_s": T * n_local / ro_s,
+                "pcie_bytes_per_vector_step": per_step_bytes,
+                "note": "one iteration with the rollout through pinned host buffers "
+                        "(ddrl_step_host / ddrl_act_host / ddrl_env_step_host), a host sync per env "
+                        "step for the host env plane; the env stepping itself is not included"}
 
     upd_avg_ms = float(np.mean(upd_ms))
     steps_per_policy = int(steps_done[-1])
@@ -323,6 +371,8 @@ def main():
             "frac_of_active_cus": achieved_tf / (PEAK_FP32_TFLOPS * active_cus / 256),
         },
     }
+    if pcie is not None:
+        result["pcie_inclusive"] = pcie
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not gnn:
         v, dt, sample = cpu_baseline(args.env, args.cpu_envs, T)
         result["cpu_baseline"] = {"value": v, "unit": "env-steps/s", "cores": 1, "kind": "port",

@@ -67,6 +67,8 @@ struct ddrl_ctx {
   GnnScratch gnn{};               // GraphNet step scratch (per-tile partial gradients, ...)
   // host-variant staging
   float *h_obs = nullptr, *h_eps = nullptr, *h_act = nullptr;
+  float *h_fw = nullptr, *h_cfrc = nullptr;
+  uint8_t* h_done = nullptr;
   std::vector<void*> allocs;
 };
 
@@ -209,7 +211,8 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
        dalloc(c, &c->d_uargs, DDRL_MAXP) || dalloc(c, &c->xchg, 8 * DDRL_MAXP) ||
        dalloc(c, &c->gx, gx_bytes(DDRL_MAXP) / sizeof(unsigned long long)) || dalloc(c, &c->err, 1) ||
        dalloc(c, &c->h_obs, (size_t)N * g.obs_full_dim) ||
-       dalloc(c, &c->h_eps, (size_t)N * g.n_agents * g.act_dim) || dalloc(c, &c->h_act, (size_t)N * 8);
+       dalloc(c, &c->h_eps, (size_t)N * g.n_agents * g.act_dim) || dalloc(c, &c->h_act, (size_t)N * 8) ||
+       dalloc(c, &c->h_fw, N) || dalloc(c, &c->h_cfrc, (size_t)N * 14 * 6) || dalloc(c, &c->h_done, N);
   if (!rc && g.model_kind == DDRL_MODEL_GNN) {
     const int np = c->pol[0].n_params;
     c->gnn.part_stride = (np + 3) & ~3;   // 16-byte aligned tile rows (float4 partial stores)
@@ -497,6 +500,32 @@ int ddrl_step_host(ddrl_ctx* c, int t, const float* obs_h, const float* eps_h, f
   if (ddrl_act(c, t, c->h_eps, c->h_act)) return -1;
   HIPCHK(hipMemcpyAsync(act_h, c->h_act, (size_t)g.n_envs * 8 * 4, hipMemcpyDeviceToHost, c->stream));
   return 0;
+}
+
+int ddrl_act_host(ddrl_ctx* c, int t, const float* eps_h, float* act_h) {
+  CHK_CTX(c);
+  if (!eps_h || !act_h) return fail("null host buffer");
+  const ddrl_cfg& g = c->cfg;
+  HIPCHK(hipMemcpyAsync(c->h_eps, eps_h, (size_t)g.n_envs * g.n_agents * g.act_dim * 4, hipMemcpyHostToDevice,
+                        c->stream));
+  if (ddrl_act(c, t, c->h_eps, c->h_act)) return -1;
+  HIPCHK(hipMemcpyAsync(act_h, c->h_act, (size_t)g.n_envs * 8 * 4, hipMemcpyDeviceToHost, c->stream));
+  return 0;
+}
+
+int ddrl_env_step_host(ddrl_ctx* c, int t, const float* fw_h, const float* cfrc_h, const uint8_t* done_h,
+                       const float* obs_h) {
+  CHK_CTX(c);
+  if (!fw_h || !cfrc_h || !obs_h) return fail("null host buffer");
+  const ddrl_cfg& g = c->cfg;
+  const size_t N = g.n_envs;
+  HIPCHK(hipMemcpyAsync(c->h_fw, fw_h, N * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->h_cfrc, cfrc_h, N * 14 * 6 * 4, hipMemcpyHostToDevice, c->stream));
+  if (done_h) HIPCHK(hipMemcpyAsync(c->h_done, done_h, N, hipMemcpyHostToDevice, c->stream));
+  // the env actions of step t are still in h_act (act_host / step_host wrote them)
+  if (ddrl_reward(c, t, c->h_fw, c->h_cfrc, c->h_act, done_h ? c->h_done : nullptr)) return -1;
+  HIPCHK(hipMemcpyAsync(c->h_obs, obs_h, N * g.obs_full_dim * 4, hipMemcpyHostToDevice, c->stream));
+  return ddrl_observe(c, c->h_obs);
 }
 
 int ddrl_gae(ddrl_ctx* c) {

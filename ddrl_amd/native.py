@@ -71,6 +71,8 @@ _SIGS = {
     "ddrl_reward": ([VP, C.c_int, VP, VP, VP, VP], C.c_int),
     "ddrl_bootstrap": ([VP], C.c_int),
     "ddrl_step_host": ([VP, C.c_int, VP, VP, VP], C.c_int),
+    "ddrl_act_host": ([VP, C.c_int, VP, VP], C.c_int),
+    "ddrl_env_step_host": ([VP, C.c_int, VP, VP, VP, VP], C.c_int),
     "ddrl_gae": ([VP], C.c_int),
     "ddrl_ppo_update": ([VP, C.c_int, C.POINTER(VP), C.POINTER(VP), C.POINTER(f32), C.c_int], C.c_int),
     "ddrl_ppo_stats": ([VP, C.c_int, VP, C.c_size_t], C.c_int),
@@ -293,6 +295,13 @@ class Context:
 
     def step_host(self, t, obs_host, eps_host, actions_host):
         _ck(self.lib.ddrl_step_host(self.h, t, _ptr(obs_host), _ptr(eps_host), _ptr(actions_host)))
+
+    def act_host(self, t, eps_host, actions_host):
+        _ck(self.lib.ddrl_act_host(self.h, t, _ptr(eps_host), _ptr(actions_host)))
+
+    def env_step_host(self, t, fw_host, cfrc_host, done_host, obs_next_host):
+        _ck(self.lib.ddrl_env_step_host(self.h, t, _ptr(fw_host), _ptr(cfrc_host), _ptr(done_host),
+                                        _ptr(obs_next_host)))
 
     def gae(self):
         _ck(self.lib.ddrl_gae(self.h))

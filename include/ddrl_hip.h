@@ -136,9 +136,20 @@ int ddrl_act(ddrl_ctx* ctx, int t, const float* eps_dev, float* actions_dev);
 int ddrl_reward(ddrl_ctx* ctx, int t, const float* fw_dev, const float* cfrc_dev,
                 const float* actions_dev, const uint8_t* done_dev);
 int ddrl_bootstrap(ddrl_ctx* ctx);
-/* Host-buffer variant of one env step (pinned buffers; hipMemcpyAsync in, actions out). */
+/* Host-buffer variants for a host-side env (MultiAgentEnv.step on host cores): pinned
+ * buffers, hipMemcpyAsync on the context's stream, asynchronous like the device calls.
+ *   step_host:     obs_host[N][D] in -> observe; eps_host in -> act(t); actions_host[N][8] out
+ *                  (the reset observation and the first action of a fragment);
+ *   act_host:      eps_host in -> act(t) on the staged observation -> actions_host out;
+ *   env_step_host: the env's answer to the actions of step t: fw_host[N], cfrc_host[N][14][6],
+ *                  done_host[N] (may be NULL) -> reward(t); obs_next_host[N][D] -> observe.
+ * A loop over t: act_host(t) (step_host for t = 0), synchronize, step the envs on the host,
+ * env_step_host(t). */
 int ddrl_step_host(ddrl_ctx* ctx, int t, const float* obs_host, const float* eps_host,
                    float* actions_host);
+int ddrl_act_host(ddrl_ctx* ctx, int t, const float* eps_host, float* actions_host);
+int ddrl_env_step_host(ddrl_ctx* ctx, int t, const float* fw_host, const float* cfrc_host,
+                       const uint8_t* done_host, const float* obs_next_host);
 
 /* Postprocessing: GAE over the fragment for every policy + advantage standardization
  * statistics (a11/a12). */

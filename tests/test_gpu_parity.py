@@ -256,3 +256,45 @@ def test_policy_forward_matches_oracle():
     _close(logits.cpu().numpy(), lr)
     _close(values.cpu().numpy(), vr)
     ctx.close()
+
+
+def test_host_buffer_loop_matches_device_loop():
+    """ddrl_step_host / ddrl_act_host / ddrl_env_step_host (pinned host buffers, the host-env
+    plane's interface) produce bit-identical records and actions to the device-buffer calls."""
+    import torch
+    from tests.gpu_harness import synthetic_inputs
+    env, n, T = "QuantrupedMultiEnv_Local", 48, 5
+    ctx_d, cfg, inst = make_ctx(env, n, T)
+    ctx_h, _, _ = make_ctx(env, n, T)
+    rng = np.random.default_rng(12)
+    filt = _filt(cfg.obs_full_dim, rng)
+    for c in (ctx_d, ctx_h):
+        init_params(c, cfg, 4)
+        c.filter_set(*filt)
+    obs, eps, fw, cfrc, done = synthetic_inputs(rng, cfg, T)
+    pin = lambda a: torch.from_numpy(np.ascontiguousarray(a)).pin_memory()
+    obs_h, eps_h, fw_h, cfrc_h, done_h = map(pin, (obs, eps, fw, cfrc, done))
+    act_h = torch.zeros((n, 8), dtype=torch.float32).pin_memory()
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    actions = torch.zeros((n, 8), dtype=torch.float32, device="cuda")
+    ctx_d.observe(dev(obs[0]))
+    for t in range(T):
+        ctx_d.act(t, dev(eps[t]), actions)
+        ctx_d.reward(t, dev(fw[t]), dev(cfrc[t]), actions, dev(done[t]))
+        ctx_d.observe(dev(obs[t + 1]))
+        if t == 0:
+            ctx_h.step_host(0, obs_h[0], eps_h[0], act_h)
+        else:
+            ctx_h.act_host(t, eps_h[t], act_h)
+        ctx_h.synchronize()                      # the host env needs the actions
+        np.testing.assert_array_equal(act_h.numpy(), actions.cpu().numpy())
+        ctx_h.env_step_host(t, fw_h[t], cfrc_h[t], done_h[t], obs_h[t + 1])
+    for c in (ctx_d, ctx_h):
+        c.bootstrap()
+        c.gae()
+    ctx_d.synchronize()
+    ctx_h.synchronize()
+    for p in range(cfg.n_policies):
+        np.testing.assert_array_equal(ctx_h.records_get(p), ctx_d.records_get(p))
+    ctx_d.close()
+    ctx_h.close()
