@@ -218,7 +218,11 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
     c->gnn.part_stride = (np + 3) & ~3;   // 16-byte aligned tile rows (float4 partial stores)
     c->gnn.grad = c->pol[0].grad;
     rc = dalloc(c, &c->gnn.part, (size_t)(DDRL_MB / 4) * c->gnn.part_stride) || dalloc(c, &c->gnn.statp, 2 * (DDRL_MB / 4) * 8) ||
-         dalloc(c, &c->gnn.normp, (np + 255) / 256) || dalloc(c, &c->gnn.bp_cur, 2);
+         dalloc(c, &c->gnn.normp, (np + 255) / 256) || dalloc(c, &c->gnn.bp_cur, 2) ||
+         dalloc(c, &c->gnn.stage, (size_t)DDRL_MB * c->pol[0].lay.stride);
+    // the fused update's row table: one entry per (minibatch step, row) of the schedule
+    c->gnn.rows_cap = (size_t)g.num_sgd_iter * c->pol[0].nb * DDRL_MB;
+    rc = rc || dalloc(c, &c->gnn.rows, c->gnn.rows_cap);
   }
   if (!rc) {
     float* tab[DDRL_MAXP] = {nullptr};
@@ -589,9 +593,13 @@ int ddrl_ppo_update(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const 
   if (c->cfg.model_kind == DDRL_MODEL_FFN)
     launch_update_ffn(c->stream, c->d_uargs, h, 128, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim, maxd, maxs,
                       c->cfg.leg_coupling, c->xchg, c->gx, c->update_split, c->err);
-  else
-    for (int step = 0; step < c->pol[0].last_steps; ++step)   // one shared policy
-      launch_step_gnn(c->stream, ua[0], h, step, 128, 1.f / c->cfg.sgd_minibatch_size, c->gnn);
+  else if (c->pol[0].last_steps > 0) {   // one shared policy
+    const int last = c->pol[0].last_steps;
+    launch_gnn_schedule(c->stream, ua[0], last, 0, c->gnn);
+    for (int step = 0; step < last; ++step)
+      launch_step_gnn(c->stream, ua[0], h, step, 128, 1.f / c->cfg.sgd_minibatch_size, c->gnn, true,
+                      step + 1 < last);
+  }
   HIPCHK(hipGetLastError());
   return 0;
 }

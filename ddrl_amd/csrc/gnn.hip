@@ -96,9 +96,13 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
     sel = gvalid ? ga.node[graph] : 0;
   } else {
     const UpdateArgs& U = ga.u;
-    const int e = ga.step / U.nb, b = ga.step - e * U.nb;
-    ridx = gvalid ? U.shuffle[U.perm[e * U.nb + b] * DDRL_MB + graph] : 0;
-    X = U.rec + (size_t)ridx * U.lay.stride + U.lay.obs;
+    if (ga.stage) {   // staged by the previous step's reduction: no dependent index loads
+      X = ga.stage + (size_t)(gvalid ? graph : 0) * U.lay.stride + U.lay.obs;
+    } else {
+      const int e = ga.step / U.nb, b = ga.step - e * U.nb;
+      ridx = gvalid ? U.shuffle[U.perm[e * U.nb + b] * DDRL_MB + graph] : 0;
+      X = U.rec + (size_t)ridx * U.lay.stride + U.lay.obs;
+    }
     sel = gvalid ? (int)X[92] : 0;
   }
   const float* xr = X + n * 23;
@@ -279,7 +283,8 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
       for (int o = 0; o < O; ++o)
         out[o] = (((hp[cc * 4 + o] + hp[(16 + cc) * 4 + o]) + hp[(32 + cc) * 4 + o]) +
                   hp[(48 + cc) * 4 + o]) + th[off.bout + o];
-      const float* rp = U.rec + (size_t)ridx * U.lay.stride;
+      const float* rp = ga.stage ? ga.stage + (size_t)(4 * tile + gg) * U.lay.stride
+                                 : U.rec + (size_t)ridx * U.lay.stride;
       if constexpr (NET == 0) {
         float act[A], ol[2 * A];
 #pragma unroll
@@ -444,9 +449,24 @@ __global__ void __launch_bounds__(256) k_gnn(GnnArgs ga) {
 }
 
 // ---- reduction over tiles: grad[p] = sum_t part[t][p] (fixed order) + norm^2 partials ----
+// Gather of the records of step `step` (rows table) into the stage, one float per thread.
+__device__ __forceinline__ float gnn_stage_load(const GnnArgs& ga, int step, int gid, int& dst) {
+  const UpdateArgs& U = ga.u;
+  const int stride = U.lay.stride;
+  dst = -1;
+  if (gid >= DDRL_MB * stride) return 0.f;
+  const int row = gid / stride, col = gid - row * stride;
+  dst = gid;
+  return U.rec[(size_t)ga.rows[(size_t)step * DDRL_MB + row] * stride + col];
+}
+
 __global__ void __launch_bounds__(256) k_gnn_reduce(GnnArgs ga, int ntiles, int n) {
   __shared__ float red[4];
   const int p = blockIdx.x * 256 + threadIdx.x;
+  // the next step's records -> stage (this step's gradient kernel has finished reading it);
+  // the loads overlap the partial-gradient loads below
+  int sdst = -1;
+  const float sv_next = ga.stage_next ? gnn_stage_load(ga, ga.step + 1, p, sdst) : 0.f;
   // all tile partials of this parameter in flight at once (a runtime-bound loop would wait
   // for each load before the next add), then summed in tile order
   float v[DDRL_MB / 4];
@@ -457,6 +477,7 @@ __global__ void __launch_bounds__(256) k_gnn_reduce(GnnArgs ga, int ntiles, int 
 #pragma unroll
   for (int t = 0; t < DDRL_MB / 4; ++t) s += v[t];
   if (p < n) ga.grad[p] = s;
+  if (sdst >= 0) ga.stage[sdst] = sv_next;
   float ss = wave_sum(s * s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
   __syncthreads();
@@ -497,6 +518,13 @@ __global__ void __launch_bounds__(256) k_gnn_adam(GnnArgs ga, int nred, int n) {
   __shared__ float scale_s;
   const UpdateArgs& U = ga.u;
   const UpdateHyper& h = ga.h;
+  // this thread's parameter state first: its loads do not depend on the clip scale and
+  // overlap the squared-norm reduction below
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  const bool pv = p < n;
+  const float g0 = pv ? ga.grad[p] : 0.f;
+  float mi = pv ? U.m[p] : 0.f, vi = pv ? U.v[p] : 0.f;
+  const float th0 = pv ? U.theta[p] : 0.f;
   if (threadIdx.x < 64) {
     // squared-norm partials of the reduction blocks: the same butterfly in every block
     float part = 0.f;
@@ -516,17 +544,38 @@ __global__ void __launch_bounds__(256) k_gnn_adam(GnnArgs ga, int nred, int n) {
   }
 done:
   __syncthreads();
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p >= n) return;
+  if (!pv) return;
   const float b1p = ga.bp_cur[0], b2p = ga.bp_cur[1];
   const float alpha = h.lr * sqrtf(1.f - b2p) / (1.f - b1p);
-  const float g = ga.grad[p] * scale_s;
-  float mi = U.m[p], vi = U.v[p];
+  const float g = g0 * scale_s;
   mi = mi + (g - mi) * (1.f - h.b1);
   vi = vi + (g * g - vi) * (1.f - h.b2);
   U.m[p] = mi;
   U.v[p] = vi;
-  U.theta[p] = U.theta[p] - (mi * alpha) / (sqrtf(vi) + h.eps);
+  U.theta[p] = th0 - (mi * alpha) / (sqrtf(vi) + h.eps);
+}
+
+// Row table of the schedule: rows[s][i] = shuffle[perm[e][b] * 128 + i], s = e * nb + b.
+__global__ void k_gnn_rows(UpdateArgs u, int n_steps, int32_t* rows) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)n_steps * DDRL_MB) return;
+  const int s = (int)(i / DDRL_MB), r = (int)(i - (size_t)s * DDRL_MB);
+  const int e = s / u.nb, b = s - e * u.nb;
+  rows[i] = u.shuffle[u.perm[e * u.nb + b] * DDRL_MB + r];
+}
+
+__global__ void k_gnn_stage(GnnArgs ga, int step) {
+  int dst;
+  const float v = gnn_stage_load(ga, step, blockIdx.x * blockDim.x + threadIdx.x, dst);
+  if (dst >= 0) ga.stage[dst] = v;
+}
+
+void launch_gnn_schedule(hipStream_t s, const UpdateArgs& u, int n_steps, int step0, const GnnScratch& sc) {
+  const size_t n = (size_t)n_steps * DDRL_MB;
+  hipLaunchKernelGGL(k_gnn_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, u, n_steps, sc.rows);
+  GnnArgs ga{};
+  ga.u = u; ga.rows = sc.rows; ga.stage = sc.stage;
+  hipLaunchKernelGGL(k_gnn_stage, dim3((DDRL_MB * u.lay.stride + 255) / 256), dim3(256), 0, s, ga, step0);
 }
 
 int gnn_param_total(int A) { return gnn_net_off(A, 1).bout + 1; }
@@ -560,17 +609,23 @@ void launch_forward_gnn(hipStream_t s, const ForwardArgs& fa) {
 }
 
 void launch_step_gnn(hipStream_t s, const UpdateArgs& u, const UpdateHyper& h, int step, int nrows, float inv_n,
-                     const GnnScratch& sc) {
+                     const GnnScratch& sc, bool staged, bool stage_next) {
   check_a(u.A);
   GnnArgs ga{};
   ga.theta = u.theta; ga.u = u; ga.h = h; ga.step = step; ga.n_graphs = nrows; ga.inv_n = inv_n;
   ga.part = sc.part; ga.part_stride = sc.part_stride; ga.statp = sc.statp; ga.normp = sc.normp;
   ga.bp_cur = sc.bp_cur; ga.grad = u.grad_out ? u.grad_out : sc.grad;
+  if (staged) {
+    ga.stage = sc.stage; ga.rows = sc.rows; ga.stage_next = stage_next ? 1 : 0;
+  }
   const int ntiles = (nrows + 3) / 4;
   const int n = gnn_param_total(u.A);
   // tiles of the critic write their statistics after the actor's: statp [2][32][8]
   hipLaunchKernelGGL((k_gnn<2, GNN_GRAD>), dim3(ntiles, 2), dim3(256), 0, s, ga);
   const int nred = (n + 255) / 256;
+#ifdef DDRL_ABL_GNN_GRAD_ONLY   // ablation build (timing only): no reduction / Adam launches
+  return;
+#endif
   hipLaunchKernelGGL(k_gnn_reduce, dim3(nred), dim3(256), 0, s, ga, ntiles, n);
   if (!u.grad_out) hipLaunchKernelGGL(k_gnn_adam, dim3(nred), dim3(256), 0, s, ga, nred, n);
 }

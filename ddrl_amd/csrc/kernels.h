@@ -161,8 +161,20 @@ struct GnnArgs {
   float* normp;                  // [reduce blocks] squared-norm partials
   float* bp_cur;                 // [2] beta powers of the current step
   float* grad;                   // reduced gradient (scratch or the DDP output)
+  // staged minibatch (fused update only): the records of this step, gathered by the previous
+  // step's reduction ([128][stride]); rows = the row table [steps][128] of the schedule
+  float* stage; const int32_t* rows; int stage_next;
 };
-struct GnnScratch { float* part; int part_stride; float* statp; float* normp; float* bp_cur; float* grad; };
+struct GnnScratch {
+  float* part; int part_stride; float* statp; float* normp; float* bp_cur; float* grad;
+  float* stage;       // [128][stride] records of the next minibatch step
+  int32_t* rows;      // [num_sgd_iter * nb][128] record row of every (step, minibatch row)
+  size_t rows_cap;    // entries of rows
+};
 int gnn_param_total(int A);
+// staged: the fused update's schedule (rows table + staged records, see gnn.hip); false for the
+// data-parallel gradient of explicit rows
 void launch_step_gnn(hipStream_t s, const UpdateArgs& u, const UpdateHyper& h, int step, int nrows, float inv_n,
-                     const GnnScratch& sc);
+                     const GnnScratch& sc, bool staged = false, bool stage_next = false);
+// the row table of a whole schedule (steps [0, n_steps)) and the staged records of step0
+void launch_gnn_schedule(hipStream_t s, const UpdateArgs& u, int n_steps, int step0, const GnnScratch& sc);

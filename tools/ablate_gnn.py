@@ -5,13 +5,14 @@
 """
 import os, subprocess, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-VARIANTS = ["", "DDRL_ABL_GNN_NO_HBWD", "DDRL_ABL_GNN_NO_HFWD", "DDRL_ABL_GNN_EMPTY"]
+VARIANTS = ["", "DDRL_ABL_GNN_NO_HBWD", "DDRL_ABL_GNN_NO_HFWD", "DDRL_ABL_GNN_EMPTY", "DDRL_ABL_GNN_GRAD_ONLY",
+            "DDRL_ABL_GNN_EMPTY -DDDRL_ABL_GNN_GRAD_ONLY"]
 
 
 def paths(v):
     from ddrl_amd import native as N
     d = os.path.dirname(N.LIB_PATH)
-    tag = v.replace("DDRL_ABL_GNN_", "").lower() or "base"
+    tag = v.replace("DDRL_ABL_GNN_", "").replace(" -D", "_").lower() or "base"
     return os.path.join(d, f"libddrl_hip_gabl_{tag}.so"), os.path.join(d, f"_build_gabl_{tag}")
 
 
@@ -39,8 +40,10 @@ def one(lib):
     ctx.synchronize()
     t0 = time.perf_counter()
     ctx.ppo_update(1, [sh], [pe], [0.2], max_steps=steps)
+    t1 = time.perf_counter()
     ctx.synchronize()
-    print(f"{(time.perf_counter() - t0) / steps * 1e6:.2f} us/step")
+    t2 = time.perf_counter()
+    print(f"{(t2 - t0) / steps * 1e6:.2f} us/step (host enqueue {(t1 - t0) / steps * 1e6:.2f} us/step)")
 
 
 if __name__ == "__main__":
