@@ -146,18 +146,21 @@ __device__ __forceinline__ void issue_rows(const float* rec, int stride, int cpr
 // stride: their LDS budget has no room for the pad)
 __host__ __device__ constexpr int stg_chunks(int stride, int A) { return A == 8 ? stride / 4 : (stride / 4) | 1; }
 
-// This lane's two rows from the staged records (padding rows hold record 0; their output
-// gradient is zeroed).  Observation columns f >= d read the record's next (finite) fields,
-// which meet the zero rows of the W1 image; their dW1 rows are never stored.
+// This lane's rows from the staged records (padding rows hold record 0; their output
+// gradient is zeroed).  Observation columns f >= d are zero (they meet the zero rows of the
+// W1 image; their dW1 rows are never stored): the generic KS1 = 12 instance (d of no exact
+// instance, e.g. the LegID env's 23) would otherwise read past the record -- past the staging
+// buffer for the last row, whatever that LDS holds -- and 0 x NaN is NaN.
 template <int A, int KS1, bool POL, int RT>
 __device__ __forceinline__ void load_row(const float* stg, int stg_stride, const RecLayout& L, const int* row_l,
-                                         RowData<A, RT>& r) {
+                                         int d, RowData<A, RT>& r) {
   const int q = (threadIdx.x & 63) >> 4;
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
     const float* rp = stg + row_l[t] * stg_stride;
 #pragma unroll
-    for (int s = 0; s < 12; ++s) r.x[t][s] = s < KS1 ? rp[L.obs + 4 * s + q] : 0.f;
+    for (int s = 0; s < 12; ++s)   // exact instances (KS1 = ceil(d / 4)) stay inside the record
+      r.x[t][s] = (s < KS1 && (KS1 < 12 || 4 * s + q < d)) ? rp[L.obs + 4 * s + q] : 0.f;
     if (POL) {
 #pragma unroll
       for (int j = 0; j < A; ++j) r.act[t][j] = rp[L.act + j];
@@ -420,7 +423,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 
   STAMP_INIT
   for (int step = U.step0; step < last; ++step) {
-    load_row<A, KS1, POL, RT>(stg, 4 * cpr_l, U.lay, row_l, cur);
+    load_row<A, KS1, POL, RT>(stg, 4 * cpr_l, U.lay, row_l, d, cur);
     // ---- forward + loss + output gradient (two row tiles) ----
     floatx4 h1[RT][4], h2[RT][4], dz[RT][4];
     float out[RT][OB], dout[RT][OB];
