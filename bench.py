@@ -70,9 +70,9 @@ def gnn_flops_per_row(A, H=64, F=19):
     return 3 * fwd + 2 * 4 * 4 * F * H * 2
 
 
-def cpu_baseline(env, n_envs=128, T=200, seed=0):
+def cpu_baseline(env, n_envs=128, T=200, seed=0, threads=1):
     """The numpy oracle on a bounded sample of the same workload (same env, same PPO
-    schedule, fewer envs), BLAS limited to one thread.  Returns env-steps/s."""
+    schedule, fewer envs), BLAS limited to `threads` threads.  Returns env-steps/s."""
     from threadpoolctl import threadpool_limits
     from oracle import ddrl_oracle as O
     from ddrl_amd.spec import make_cfg
@@ -86,7 +86,7 @@ def cpu_baseline(env, n_envs=128, T=200, seed=0):
     eps = rng.normal(size=(T, n_envs, cfg.n_agents, A)).astype(np.float32)
     fw = rng.normal(size=(T, n_envs)).astype(np.float32)
     cfrc = rng.normal(size=(T, n_envs, 14, 6)).astype(np.float32)
-    with threadpool_limits(limits=1):
+    with threadpool_limits(limits=threads):
         t0 = time.perf_counter()
         rs = O.RunningStat((cfg.obs_full_dim,))
         rec = [dict(obs=[], act=[], logits=[], logp=[], vf=[]) for _ in range(P)]
@@ -248,9 +248,19 @@ def main():
                 upd_ms.append(ev_upd[0].elapsed_time(ev_upd[1]))
                 steps_done.append(pe.size)
             return
-        shuffles = [torch.randperm(R[p], device=stream.device, generator=gen, dtype=torch.int32) for p in range(P)]
-        perms = [torch.stack([torch.randperm(nb[p], device=stream.device, generator=gen, dtype=torch.int32)
-                              for _ in range(E)]).contiguous() for p in range(P)]
+        # SampleBatch.shuffle + per-epoch minibatch permutations of every policy: one batched
+        # argsort of fp64 uniforms each (policies of one env have equal batch sizes)
+        if len(set(R)) == 1:
+            dev = stream.device
+            sh_all = torch.rand((P, R[0]), device=dev, generator=gen, dtype=torch.float64).argsort(dim=1)
+            pe_all = torch.rand((P, E, nb[0]), device=dev, generator=gen, dtype=torch.float64).argsort(dim=2)
+            sh_all, pe_all = sh_all.to(torch.int32), pe_all.to(torch.int32)
+            shuffles = [sh_all[p] for p in range(P)]
+            perms = [pe_all[p] for p in range(P)]
+        else:
+            shuffles = [torch.randperm(R[p], device=stream.device, generator=gen, dtype=torch.int32) for p in range(P)]
+            perms = [torch.stack([torch.randperm(nb[p], device=stream.device, generator=gen, dtype=torch.int32)
+                                  for _ in range(E)]).contiguous() for p in range(P)]
         ev_upd[0].record(stream)
         ctx.ppo_update((1 << P) - 1, shuffles, perms, kl)
         ev_upd[1].record(stream)
@@ -377,6 +387,12 @@ def main():
         v, dt, sample = cpu_baseline(args.env, args.cpu_envs, T)
         result["cpu_baseline"] = {"value": v, "unit": "env-steps/s", "cores": 1, "kind": "port",
                                   "sample": sample + f"; {dt:.1f} s", "host_cpus": os.cpu_count()}
+        # the same sample with BLAS on this job's share of the host cores
+        # (OMP_NUM_THREADS on the GPU box; the machine's CPUs are shared between jobs)
+        nthr = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count())
+        v2, dt2, _ = cpu_baseline(args.env, args.cpu_envs, T, threads=nthr)
+        result["cpu_baseline_all_cores"] = {"value": v2, "unit": "env-steps/s", "cores": nthr, "kind": "port",
+                                            "sample": f"same sample; {dt2:.1f} s"}
     if rank == 0:
         print(json.dumps(result), flush=True)
     ctx.close()

@@ -424,11 +424,13 @@ int ddrl_observe(ddrl_ctx* c, const float* obs) {
                      g.filter_update, g.filter_enabled, c->f_dn, c->f_dM, c->f_dS);
   const float clip = g.filter_enabled ? g.filter_clip : 0.f;
   if (g.policy_filter) launch_policy_filter(c->stream, c->route, obs, c->f_normc, clip, c->zs, c->pf, 1);
+  const FilterCount fc{c->f_n, c->f_dn, g.filter_enabled && g.filter_update ? g.n_envs : 0};
   if (g.model_kind == DDRL_MODEL_FFN)
-    launch_observe_ffn(c->stream, c->route, obs, c->f_normc, clip, c->stage_tab, g.policy_filter ? c->pf : nullptr);
+    launch_observe_ffn(c->stream, c->route, obs, c->f_normc, clip, c->stage_tab, g.policy_filter ? c->pf : nullptr,
+                       fc);
   else
     launch_observe_gnn(c->stream, c->route, obs, c->f_normc, g.filter_enabled ? g.filter_clip : 0.f,
-                       c->pol[0].stage);
+                       c->pol[0].stage, fc);
   HIPCHK(hipGetLastError());
   return 0;
 }

@@ -15,6 +15,49 @@
 
 #pragma clang fp contract(off)
 
+// The record loads of a chunk of GAE_U time steps are issued one chunk ahead of the
+// recursion (the stores of adv / vt may alias them as far as the compiler knows, so it would
+// otherwise wait for every load in turn: one memory round trip per time step).
+#define GAE_U 8
+struct GaeChunk { float v[GAE_U], r[GAE_U]; bool d[GAE_U]; };
+
+__device__ __forceinline__ void gae_load(const GaeArgs& g, int c, int e, int t0, GaeChunk& ch) {
+#pragma unroll
+  for (int u = 0; u < GAE_U; ++u) {
+    const int t = t0 - u;
+    if (t >= 0) {
+      const float* rp = g.rec + ((size_t)t * g.C + c) * g.lay.stride;
+      ch.v[u] = rp[g.lay.vf];
+      ch.r[u] = rp[g.lay.rew];
+      ch.d[u] = g.done_tn[(size_t)t * g.N + e] != 0;
+    }
+  }
+}
+
+__device__ __forceinline__ void gae_run(const GaeArgs& g, int c, int t0, const GaeChunk& ch, double& acc,
+                                        double& nextv, double& s1, double& s2) {
+  const double gl = g.gamma * g.lambda_;
+#pragma unroll
+  for (int u = 0; u < GAE_U; ++u) {
+    const int t = t0 - u;
+    if (t < 0) break;
+    if (ch.d[u]) {
+      acc = 0.0;
+      nextv = 0.0;
+    }
+    const double v = (double)ch.v[u];
+    const double delta = (double)ch.r[u] + g.gamma * nextv - v;
+    acc = delta + gl * acc;
+    const float a32 = (float)acc;
+    float* rp = g.rec + ((size_t)t * g.C + c) * g.lay.stride;
+    rp[g.lay.adv] = a32;
+    rp[g.lay.vt] = (float)(acc + v);
+    s1 += (double)a32;
+    s2 += (double)a32 * (double)a32;
+    nextv = v;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_gae(GaeArgs g) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   double s1 = 0.0, s2 = 0.0;
@@ -22,23 +65,16 @@ __global__ void __launch_bounds__(256) k_gae(GaeArgs g) {
     const int e = c / g.k;
     double acc = 0.0;
     double nextv = (double)g.last_v[c];
-    const double gl = g.gamma * g.lambda_;
-    for (int t = g.T - 1; t >= 0; --t) {
-      float* rp = g.rec + ((size_t)t * g.C + c) * g.lay.stride;
-      const bool done = g.done_tn[(size_t)t * g.N + e] != 0;
-      if (done) {
-        acc = 0.0;
-        nextv = 0.0;
-      }
-      const double v = (double)rp[g.lay.vf];
-      const double delta = (double)rp[g.lay.rew] + g.gamma * nextv - v;
-      acc = delta + gl * acc;
-      const float a32 = (float)acc;
-      rp[g.lay.adv] = a32;
-      rp[g.lay.vt] = (float)(acc + v);
-      s1 += (double)a32;
-      s2 += (double)a32 * (double)a32;
-      nextv = v;
+    const int nch = (g.T + GAE_U - 1) / GAE_U;
+    GaeChunk a, b;
+    gae_load(g, c, e, g.T - 1, a);
+    for (int k = 0; k < nch; k += 2) {
+      const int ta = g.T - 1 - k * GAE_U, tb = ta - GAE_U;
+      if (k + 1 < nch) gae_load(g, c, e, tb, b);
+      gae_run(g, c, ta, a, acc, nextv, s1, s2);
+      if (k + 1 >= nch) break;
+      if (k + 2 < nch) gae_load(g, c, e, tb - GAE_U, a);
+      gae_run(g, c, tb, b, acc, nextv, s1, s2);
     }
   }
   __shared__ double red[2][4];

@@ -40,9 +40,11 @@ struct RouteArgs {
 void launch_filter_push(hipStream_t s, const float* obs, int N, int D, double* n_run, double* M,
                         double* S, double* normc, int update, int enabled, double* dn, double* dM,
                         double* dS);
+// the batch count of the env-side filter push, added by the observe kernel
+struct FilterCount { double* n_run; double* dn; int count; };
 // pf: per-policy RLlib MeanStdFilter state (PF_* layout, nullptr when disabled)
 void launch_observe_ffn(hipStream_t s, const RouteArgs& ra, const float* obs, const double* normc,
-                        float clip, float* const* stage, const double* pf);
+                        float clip, float* const* stage, const double* pf, const FilterCount& fc);
 // per-policy filter: statistics of the env-normalized observation columns, then the
 // RunningStat update + normalization constants of every policy column
 #define PF_N 0
@@ -56,7 +58,7 @@ void launch_observe_ffn(hipStream_t s, const RouteArgs& ra, const float* obs, co
 void launch_policy_filter(hipStream_t s, const RouteArgs& ra, const float* obs, const double* normc, float clip,
                           double* zs, double* pf, int update);
 void launch_observe_gnn(hipStream_t s, const RouteArgs& ra, const float* obs, const double* normc,
-                        float clip, float* stage_x /*[N][4][23]*/);
+                        float clip, float* stage_x /*[N][4][23]*/, const FilterCount& fc);
 
 // ---- act (rollout forward + sample) ----
 struct ActArgs {

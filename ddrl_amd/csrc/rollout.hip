@@ -68,17 +68,21 @@ __global__ void __launch_bounds__(256) k_filter_push(const float* __restrict__ o
   }
 }
 
-__global__ void k_filter_count(double* n_run, double* dn, int N) {
-  n_run[0] += (double)N;
-  dn[0] += (double)N;
-}
-
 void launch_filter_push(hipStream_t s, const float* obs, int N, int D, double* n_run, double* M,
                         double* S, double* normc, int update, int enabled, double* dn, double* dM,
                         double* dS) {
   hipLaunchKernelGGL(k_filter_push, dim3(D), dim3(256), 0, s, obs, N, D, n_run, M, S, normc,
                      update, enabled, dn, dM, dS);
-  if (enabled && update) hipLaunchKernelGGL(k_filter_count, dim3(1), dim3(1), 0, s, n_run, dn, N);
+}
+
+// The running count of the env-side filter advances after every column of k_filter_push has
+// read it: the observe kernel that follows adds the batch (FilterCount: count = N, or 0 when
+// the filter did not push).
+__device__ __forceinline__ void filter_count(const FilterCount& fc) {
+  if (fc.count && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    fc.n_run[0] += (double)fc.count;
+    fc.dn[0] += (double)fc.count;
+  }
 }
 
 __device__ __forceinline__ double norm_obs_d(float x, const double* normc, int idx, float clip) {
@@ -95,7 +99,8 @@ __device__ __forceinline__ float norm_obs(float x, const double* normc, int idx,
 // a1: per-agent gather of the normalized observation into stage[p][c][f].
 __global__ void k_observe_ffn(RouteArgs ra, const float* __restrict__ obs,
                               const double* __restrict__ normc, float clip, float* const* stage_tab,
-                              const double* __restrict__ pf) {
+                              const double* __restrict__ pf, FilterCount fc) {
+  filter_count(fc);
   const int p = blockIdx.y;
   const PolicyRoute& pr = ra.pol[p];
   const int C = ra.N * pr.k;
@@ -117,11 +122,11 @@ __global__ void k_observe_ffn(RouteArgs ra, const float* __restrict__ obs,
 }
 
 void launch_observe_ffn(hipStream_t s, const RouteArgs& ra, const float* obs, const double* normc,
-                        float clip, float* const* stage, const double* pf) {
+                        float clip, float* const* stage, const double* pf, const FilterCount& fc) {
   int maxw = 0;
   for (int p = 0; p < ra.P; ++p) maxw = max(maxw, ra.N * ra.pol[p].k * ra.pol[p].d);
   dim3 grid((maxw + 255) / 256, ra.P);
-  hipLaunchKernelGGL(k_observe_ffn, grid, dim3(256), 0, s, ra, obs, normc, clip, stage, pf);
+  hipLaunchKernelGGL(k_observe_ffn, grid, dim3(256), 0, s, ra, obs, normc, clip, stage, pf, fc);
 }
 
 // ------------------------------------------------------------------------------------
@@ -203,7 +208,9 @@ void launch_policy_filter(hipStream_t s, const RouteArgs& ra, const float* obs, 
 
 // a3: graph observation X[env][node] = [normalized 19 features | ego quaternion (raw obs)].
 __global__ void k_observe_gnn(RouteArgs ra, const float* __restrict__ obs,
-                              const double* __restrict__ normc, float clip, float* __restrict__ X) {
+                              const double* __restrict__ normc, float clip, float* __restrict__ X,
+                              FilterCount fc) {
+  filter_count(fc);
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= ra.N * 4) return;
   const int e = gid >> 2, n = gid & 3;
@@ -225,9 +232,9 @@ __global__ void k_observe_gnn(RouteArgs ra, const float* __restrict__ obs,
 }
 
 void launch_observe_gnn(hipStream_t s, const RouteArgs& ra, const float* obs, const double* normc,
-                        float clip, float* stage_x) {
+                        float clip, float* stage_x, const FilterCount& fc) {
   hipLaunchKernelGGL(k_observe_gnn, dim3((ra.N * 4 + 255) / 256), dim3(256), 0, s, ra, obs, normc,
-                     clip, stage_x);
+                     clip, stage_x, fc);
 }
 
 // ------------------------------------------------------------------------------------
@@ -330,58 +337,57 @@ void launch_act_ffn(hipStream_t s, const RouteArgs& ra, const ActArgs& aa) {
 // ------------------------------------------------------------------------------------
 // a8: per-leg (or global / normalized) reward of each agent; fp64 like the reference.
 // ------------------------------------------------------------------------------------
+// One thread per (env, agent): the agent's control cost and its bodies' contact cost.
 __global__ void k_reward(RewardArgs ra, const float* __restrict__ fw, const float* __restrict__ cfrc,
                          const float* __restrict__ actions, const uint8_t* __restrict__ done,
                          uint8_t* __restrict__ done_tn) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= ra.N) return;
+  const int na = ra.n_agents;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= ra.N * na) return;
+  const int e = gid / na, j = gid - e * na;
   const float* cf = cfrc + (size_t)e * 14 * 6;
   const float* a8 = actions + (size_t)e * 8;
   const double fwd = fw[e];
-  const int na = ra.n_agents;
-  double ctrl_all = 0.0, contact_all = 0.0;
+  double r;
   if (ra.mode == 1) {
+    double ctrl_all = 0.0, contact_all = 0.0;
     for (int i = 0; i < 8; ++i) ctrl_all += (double)a8[i] * a8[i];
     for (int i = 0; i < 14 * 6; ++i) {
       const double v = fmin(fmax((double)cf[i], -1.0), 1.0);
       contact_all += v * v;
     }
     contact_all *= ra.contact_w;
-  }
-  for (int j = 0; j < na; ++j) {
-    double r;
-    if (ra.mode == 1) {
-      r = (fwd - ra.ctrl_w * ctrl_all - contact_all) / na;
-    } else {
-      double ctrl = 0.0;
-      for (int i = 0; i < ra.n_act[j]; ++i) {
-        const double a = a8[ra.act_index[j][i]];
-        ctrl += a * a;
-      }
-      double contact = 0.0;
-      for (int b = 0; b < ra.n_contact[j]; ++b) {
-        const float* body = cf + ra.contact_index[j][b] * 6;
-        double sb = 0.0;
-        for (int k = 0; k < 6; ++k) {
-          const double v = fmin(fmax((double)body[k], -1.0), 1.0);
-          sb += ra.contact_w * v * v * ra.contact_weight[j][b];
-        }
-        contact += sb;
-      }
-      r = ra.mode == 2 ? fwd - na * (ra.ctrl_w * ctrl + contact)
-                       : fwd / na - ra.ctrl_w * ctrl - contact;
+    r = (fwd - ra.ctrl_w * ctrl_all - contact_all) / na;
+  } else {
+    double ctrl = 0.0;
+    for (int i = 0; i < ra.n_act[j]; ++i) {
+      const double a = a8[ra.act_index[j][i]];
+      ctrl += a * a;
     }
-    const int p = ra.policy_of_agent[j], slot = ra.slot_of_agent[j];
-    const size_t C = (size_t)ra.N * ra.k[p];
-    float* rp = ra.rec[p] + ((size_t)ra.t * C + (size_t)e * ra.k[p] + slot) * ra.lay[p].stride;
-    rp[ra.lay[p].rew] = (float)r;
+    double contact = 0.0;
+    for (int b = 0; b < ra.n_contact[j]; ++b) {
+      const float* body = cf + ra.contact_index[j][b] * 6;
+      double sb = 0.0;
+      for (int k = 0; k < 6; ++k) {
+        const double v = fmin(fmax((double)body[k], -1.0), 1.0);
+        sb += ra.contact_w * v * v * ra.contact_weight[j][b];
+      }
+      contact += sb;
+    }
+    r = ra.mode == 2 ? fwd - na * (ra.ctrl_w * ctrl + contact)
+                     : fwd / na - ra.ctrl_w * ctrl - contact;
   }
-  done_tn[(size_t)ra.t * ra.N + e] = done ? done[e] : 0;
+  const int p = ra.policy_of_agent[j], slot = ra.slot_of_agent[j];
+  const size_t C = (size_t)ra.N * ra.k[p];
+  float* rp = ra.rec[p] + ((size_t)ra.t * C + (size_t)e * ra.k[p] + slot) * ra.lay[p].stride;
+  rp[ra.lay[p].rew] = (float)r;
+  if (j == 0) done_tn[(size_t)ra.t * ra.N + e] = done ? done[e] : 0;
 }
 
 void launch_reward(hipStream_t s, const RewardArgs& ra, const float* fw, const float* cfrc,
                    const float* actions, const uint8_t* done, uint8_t* done_tn) {
-  hipLaunchKernelGGL(k_reward, dim3((ra.N + 255) / 256), dim3(256), 0, s, ra, fw, cfrc, actions,
+  const int n = ra.N * ra.n_agents;
+  hipLaunchKernelGGL(k_reward, dim3((n + 255) / 256), dim3(256), 0, s, ra, fw, cfrc, actions,
                      done, done_tn);
 }
 
