@@ -224,12 +224,10 @@ def main():
         done = syn.dones_for_fragment()
         if host_io:
             rollout_host_io(done)
+            ctx.bootstrap()
         else:
-            for t in range(T):
-                ctx.act(t, syn.eps[t], syn.actions)
-                ctx.reward(t, syn.fw[t], syn.cfrc[t], syn.actions, done[t])
-                ctx.observe(syn.obs[t + 1])
-        ctx.bootstrap()
+            # T x (act, reward, observe) + bootstrap in one C-ABI call (device-resident env data)
+            ctx.rollout_fragment(syn.obs, syn.eps, syn.fw, syn.cfrc, done, syn.actions)
         ctx.gae()
         if ddp:
             nonlocal filter_base

@@ -496,6 +496,21 @@ int ddrl_reward(ddrl_ctx* c, int t, const float* fw, const float* cfrc, const fl
   return 0;
 }
 
+int ddrl_rollout_fragment(ddrl_ctx* c, const float* obs, const float* eps, const float* fw, const float* cfrc,
+                          const uint8_t* done, float* actions) {
+  CHK_CTX(c);
+  if (!obs || !eps || !fw || !cfrc || !actions) return fail("null rollout buffer");
+  const ddrl_cfg& g = c->cfg;
+  const size_t N = g.n_envs;
+  for (int t = 0; t < g.frag_len; ++t) {
+    if (ddrl_act(c, t, eps + (size_t)t * N * g.n_agents * g.act_dim, actions)) return -1;
+    if (ddrl_reward(c, t, fw + (size_t)t * N, cfrc + (size_t)t * N * 14 * 6, actions, done ? done + (size_t)t * N : nullptr))
+      return -1;
+    if (ddrl_observe(c, obs + (size_t)(t + 1) * N * g.obs_full_dim)) return -1;
+  }
+  return ddrl_bootstrap(c);
+}
+
 int ddrl_step_host(ddrl_ctx* c, int t, const float* obs_h, const float* eps_h, float* act_h) {
   CHK_CTX(c);
   const ddrl_cfg& g = c->cfg;

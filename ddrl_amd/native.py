@@ -72,6 +72,7 @@ _SIGS = {
     "ddrl_bootstrap": ([VP], C.c_int),
     "ddrl_step_host": ([VP, C.c_int, VP, VP, VP], C.c_int),
     "ddrl_act_host": ([VP, C.c_int, VP, VP], C.c_int),
+    "ddrl_rollout_fragment": ([VP, VP, VP, VP, VP, VP, VP], C.c_int),
     "ddrl_env_step_host": ([VP, C.c_int, VP, VP, VP, VP], C.c_int),
     "ddrl_gae": ([VP], C.c_int),
     "ddrl_ppo_update": ([VP, C.c_int, C.POINTER(VP), C.POINTER(VP), C.POINTER(f32), C.c_int], C.c_int),
@@ -295,6 +296,10 @@ class Context:
 
     def step_host(self, t, obs_host, eps_host, actions_host):
         _ck(self.lib.ddrl_step_host(self.h, t, _ptr(obs_host), _ptr(eps_host), _ptr(actions_host)))
+
+    def rollout_fragment(self, obs_dev, eps_dev, fw_dev, cfrc_dev, done_dev, actions_dev):
+        _ck(self.lib.ddrl_rollout_fragment(self.h, _ptr(obs_dev), _ptr(eps_dev), _ptr(fw_dev), _ptr(cfrc_dev),
+                                           _ptr(done_dev), _ptr(actions_dev)))
 
     def act_host(self, t, eps_host, actions_host):
         _ck(self.lib.ddrl_act_host(self.h, t, _ptr(eps_host), _ptr(actions_host)))

@@ -136,6 +136,14 @@ int ddrl_act(ddrl_ctx* ctx, int t, const float* eps_dev, float* actions_dev);
 int ddrl_reward(ddrl_ctx* ctx, int t, const float* fw_dev, const float* cfrc_dev,
                 const float* actions_dev, const uint8_t* done_dev);
 int ddrl_bootstrap(ddrl_ctx* ctx);
+/* A whole fragment over device-resident env data (a device env, replayed transitions, the
+ * synthetic benchmark): for t in [0, T): act(t), reward(t), observe(obs_dev[t + 1]); then
+ * bootstrap.  Expects observe(obs_dev[0]) to have been called.  Layouts: obs_dev[T+1][N][D],
+ * eps_dev[T][N][n_agents][A], fw_dev[T][N], cfrc_dev[T][N][14][6], done_dev[T][N] (may be
+ * NULL), actions_dev[N][8] (scratch: the env actions of the last step).  One call instead of
+ * 3 T host calls: the per-step launches stay in C++. */
+int ddrl_rollout_fragment(ddrl_ctx* ctx, const float* obs_dev, const float* eps_dev, const float* fw_dev,
+                          const float* cfrc_dev, const uint8_t* done_dev, float* actions_dev);
 /* Host-buffer variants for a host-side env (MultiAgentEnv.step on host cores): pinned
  * buffers, hipMemcpyAsync on the context's stream, asynchronous like the device calls.
  *   step_host:     obs_host[N][D] in -> observe; eps_host in -> act(t); actions_host[N][8] out

@@ -298,3 +298,40 @@ def test_host_buffer_loop_matches_device_loop():
         np.testing.assert_array_equal(ctx_h.records_get(p), ctx_d.records_get(p))
     ctx_d.close()
     ctx_h.close()
+
+
+def test_rollout_fragment_matches_step_loop():
+    """ddrl_rollout_fragment (T x act / reward / observe + bootstrap in one call) produces the
+    same records, bootstrap values and filter state as the per-step calls."""
+    import torch
+    from tests.gpu_harness import synthetic_inputs
+    env, n, T = "QuantrupedMultiEnv_FullyDecentral", 40, 6
+    ctx_a, cfg, inst = make_ctx(env, n, T)
+    ctx_b, _, _ = make_ctx(env, n, T)
+    rng = np.random.default_rng(21)
+    filt = _filt(cfg.obs_full_dim, rng)
+    for c in (ctx_a, ctx_b):
+        init_params(c, cfg, 5)
+        c.filter_set(*filt)
+    obs, eps, fw, cfrc, done = synthetic_inputs(rng, cfg, T)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    obs_d, eps_d, fw_d, cfrc_d, done_d = map(dev, (obs, eps, fw, cfrc, done))
+    act_a = torch.zeros((n, 8), dtype=torch.float32, device="cuda")
+    act_b = torch.zeros((n, 8), dtype=torch.float32, device="cuda")
+    ctx_a.observe(obs_d[0])
+    for t in range(T):
+        ctx_a.act(t, eps_d[t], act_a)
+        ctx_a.reward(t, fw_d[t], cfrc_d[t], act_a, done_d[t])
+        ctx_a.observe(obs_d[t + 1])
+    ctx_a.bootstrap()
+    ctx_b.observe(obs_d[0])
+    ctx_b.rollout_fragment(obs_d, eps_d, fw_d, cfrc_d, done_d, act_b)
+    ctx_a.synchronize()
+    ctx_b.synchronize()
+    for p in range(cfg.n_policies):
+        np.testing.assert_array_equal(ctx_b.records_get(p), ctx_a.records_get(p))
+        np.testing.assert_array_equal(ctx_b.last_values_get(p), ctx_a.last_values_get(p))
+    fa, fb = ctx_a.filter_get(), ctx_b.filter_get()
+    assert fa[0] == fb[0] and np.array_equal(fa[1], fb[1]) and np.array_equal(fa[2], fb[2])
+    ctx_a.close()
+    ctx_b.close()
