@@ -736,6 +736,15 @@ int ddrl_last_values_get(ddrl_ctx* c, int pid, float* host, size_t n) {
   return 0;
 }
 
+int ddrl_last_values_set(ddrl_ctx* c, int pid, const float* host, size_t n) {
+  CHK_CTX(c);
+  if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
+  if (n != (size_t)c->pol[pid].C) return fail("last value count mismatch");
+  HIPCHK(hipMemcpyAsync(c->pol[pid].last_v, host, n * 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
 int ddrl_done_set(ddrl_ctx* c, const uint8_t* host, size_t n) {
   CHK_CTX(c);
   if (n != (size_t)c->cfg.frag_len * c->cfg.n_envs) return fail("done buffer size mismatch");

@@ -86,6 +86,7 @@ _SIGS = {
     "ddrl_adv_norm_get": ([VP, C.c_int, VP], C.c_int),
     "ddrl_adv_norm_set": ([VP, C.c_int, f32, f32], C.c_int),
     "ddrl_last_values_get": ([VP, C.c_int, VP, C.c_size_t], C.c_int),
+    "ddrl_last_values_set": ([VP, C.c_int, VP, C.c_size_t], C.c_int),
     "ddrl_done_set": ([VP, VP, C.c_size_t], C.c_int),
 }
 
@@ -276,6 +277,10 @@ class Context:
         a = np.empty(self.layout[pid]["C"], np.float32)
         _ck(self.lib.ddrl_last_values_get(self.h, pid, a.ctypes.data, a.size))
         return a
+
+    def last_values_set(self, pid, values):
+        a = np.ascontiguousarray(values, np.float32)
+        _ck(self.lib.ddrl_last_values_set(self.h, pid, a.ctypes.data, a.size))
 
     def done_set(self, done_tn):
         a = np.ascontiguousarray(done_tn, np.uint8)

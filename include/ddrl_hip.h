@@ -200,8 +200,9 @@ int ddrl_records_set(ddrl_ctx* ctx, int pid, const float* host, size_t n_floats)
 /* Advantage standardization constants {mean, max(1e-4, std)} of policy pid. */
 int ddrl_adv_norm_get(ddrl_ctx* ctx, int pid, float* host2);
 int ddrl_adv_norm_set(ddrl_ctx* ctx, int pid, float mean, float denom);
-/* Bootstrap values V(s_T) of policy pid, C floats. */
+/* Bootstrap values V(s_T) of policy pid, C floats (set: for a replayed batch). */
 int ddrl_last_values_get(ddrl_ctx* ctx, int pid, float* host, size_t n);
+int ddrl_last_values_set(ddrl_ctx* ctx, int pid, const float* host, size_t n);
 /* Episode-end flags of the fragment, [T][N] bytes (normally written by ddrl_reward). */
 int ddrl_done_set(ddrl_ctx* ctx, const uint8_t* host, size_t n);
 

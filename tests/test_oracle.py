@@ -276,3 +276,49 @@ def test_graph_observation_and_quaternion():
     np.testing.assert_allclose(q, [0, 0, np.sin(0.3), np.cos(0.3)], atol=1e-12)
     adj = O.ring_adjacency()
     assert adj.sum() == 8 and (adj.sum(0) == 2).all()
+
+
+def test_oracle_reproduces_golden_vectors():
+    """The committed oracle vectors (tests/golden/oracle_golden.npz, made by
+    tests/golden/make_oracle_golden.py) are reproduced from their stored inputs: forward,
+    sampling, GAE + standardization, and one PPO minibatch (gradient, clip + Adam) for the
+    fcnet, "cup" and GraphNet models."""
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "oracle_golden.npz"))
+    close = lambda a, b: np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-7)
+    shapes = O.ffn_param_shapes(35, 4)
+    p = O.unpack(z["ffn_params"], shapes)
+    logits, value, _ = O.ffn_forward(p, z["ffn_obs"])
+    close(logits, z["ffn_logits"])
+    close(value, z["ffn_value"])
+    act = O.dg_sample(logits, z["ffn_eps"])
+    close(act, z["ffn_actions"])
+    close(O.dg_logp(logits, act), z["ffn_logp"])
+    adv, vt = O.gae_fragment(z["gae_rew"], z["gae_vf"], z["gae_dones"], z["gae_last_v"])
+    close(adv, z["gae_adv"])
+    close(vt, z["gae_vt"])
+    _, mean, std = O.standardize(adv.reshape(-1))
+    close(np.array([mean, max(np.float32(1e-4), std)], np.float32), z["gae_norm"])
+    for model, pre, shp in (("ffn", "ffn_step_", shapes), ("cup", "cup_", O.cup_param_shapes(19, 2)),
+                            ("gnn", "gnn_", O.gnn_param_shapes(4))):
+        params = O.unpack(z[pre + "params"] if model == "ffn" else z[pre + "params"], shp)
+        b = {k[len(pre):]: z[k] for k in z.files if k.startswith(pre)}
+        if model == "ffn":
+            logits, value, cache = O.ffn_forward(params, b["obs"])
+        elif model == "cup":
+            logits, value, cache = O.cup_forward(params, b["obs"], b["leg"])
+            close(logits, z["cup_fwd_logits"])
+        else:
+            logits, value, cache = O.gnn_forward(params, b["X"], b["node_idx"])
+            close(logits, z["gnn_fwd_logits"])
+            close(value, z["gnn_fwd_value"])
+        dl, dv, st = O.ppo_loss_rows(logits, value, b["actions"], b["logits"], b["logp"], b["vf_preds"],
+                                     b["adv"], b["vt"], np.float32(0.3 if model == "ffn" else 0.2))
+        g = {"ffn": O.ffn_backward, "cup": O.cup_backward, "gnn": O.gnn_backward}[model](params, cache, dl, dv)
+        flat = np.concatenate([g[n].reshape(-1) for n, _ in shp])
+        close(flat, z[pre + "grad"])
+        clipped, gn = O.clip_by_global_norm([flat], 0.5)
+        new = O.Adam(flat.size).apply(O.pack(params, shp), clipped[0])
+        close(new, z[pre + "new_params"])
+        close(np.array([st["total_loss"], st["policy_loss"], st["vf_loss"], st["kl"], st["entropy"],
+                        st["vf_explained_var"], gn], np.float32), z[pre + "stats"])
