@@ -50,7 +50,20 @@ ROLLOUT_ENVS = [
 
 @pytest.mark.parametrize("env,n,T", ROLLOUT_ENVS)
 def test_rollout_gae_parity(env, n, T):
-    ctx, cfg, inst = make_ctx(env, n, T)
+    _rollout_gae_parity(env, n, T, None)
+
+
+@pytest.mark.parametrize("env,n,T", [("QuantrupedMultiEnv_FullyDecentral", 24, 4),
+                                     ("QuantrupedMultiEnv_Local", 20, 3),
+                                     ("QuantrupedMultiEnv_Centralized", 16, 3)])
+def test_rollout_gae_parity_target_velocity(env, n, T):
+    """TVel variants (quantruped_v3.py:351-399): the 44th observation column
+    (body_target_x_vel) is routed to every policy's input."""
+    _rollout_gae_parity(env, n, T, {"env_config": {"target_velocity": [1.0]}})
+
+
+def _rollout_gae_parity(env, n, T, config):
+    ctx, cfg, inst = make_ctx(env, n, T, config)
     rng = np.random.default_rng(11)
     params = init_params(ctx, cfg, 3)
     orc, norms, a_gpu, a_orc = run_rollout(ctx, cfg, inst, params, rng, _filt(cfg.obs_full_dim, rng), T)
@@ -123,15 +136,21 @@ def _params_close(got, ref, lr, steps, msg):
     assert diff.max() <= 2 * lr * steps + 1e-5, f"{msg}: max deviation {diff.max():.3g}"
 
 
-@pytest.mark.parametrize("env,n,T,steps", [
-    ("QuantrupedMultiEnv_Local", 64, 6, 3),
-    ("QuantrupedMultiEnv_SharedDecentral", 32, 4, 2),
-    ("QuantrupedMultiEnv_Centralized", 48, 8, 2),
-    ("QuantrupedMultiEnv_SharedDecentralLegID", 32, 4, 2),
+TVEL = {"env_config": {"target_velocity": [1.0]}}   # obs 44: body_target_x_vel appended
+
+
+@pytest.mark.parametrize("env,n,T,steps,config", [
+    ("QuantrupedMultiEnv_Local", 64, 6, 3, None),
+    ("QuantrupedMultiEnv_SharedDecentral", 32, 4, 2, None),
+    ("QuantrupedMultiEnv_Centralized", 48, 8, 2, None),
+    ("QuantrupedMultiEnv_SharedDecentralLegID", 32, 4, 2, None),
+    ("QuantrupedMultiEnv_TwoSides", 33, 4, 2, None),             # A = 4, d = 27; ragged envs
+    ("QuantrupedMultiEnv_FullyDecentral", 37, 5, 2, TVEL),        # d = 20 (TVel), 4 policies
+    ("QuantrupedMultiEnv_Local", 40, 4, 2, TVEL),                 # d = 36 (TVel)
 ])
-def test_ppo_update_parity(env, n, T, steps):
+def test_ppo_update_parity(env, n, T, steps, config):
     import torch
-    ctx, cfg, inst = make_ctx(env, n, T)
+    ctx, cfg, inst = make_ctx(env, n, T, config)
     rng = np.random.default_rng(5)
     params = init_params(ctx, cfg, 7, head_scale=1.0)
     orc, norms, _, _ = run_rollout(ctx, cfg, inst, params, rng, _filt(cfg.obs_full_dim, rng), T)
