@@ -1,0 +1,119 @@
+"""Full-size checks (BASELINE C2/C3 workload: QuantrupedMultiEnv_Local at 4096 envs, T = 200,
+819,200 records per policy) through size-independent properties, on the GPU:
+
+  * sampled rows of the rollout records agree with the oracle recomputed from the row's own
+    stored observation (forward), action (logp) and the policy's weights;
+  * sampled GAE chains (whole T = 200 fragments, with episode ends) agree with the oracle's
+    lfilter recursion on the stored rewards / values / dones;
+  * the standardization constants equal the fp64 statistics of all 819,200 advantages;
+  * the first fused minibatch step at full size equals the oracle's step on that minibatch,
+    and 200 further steps keep every parameter finite.
+
+Tolerances: rows 1e-5 relative + 2e-5 absolute; adv / vt 1e-5 relative + 2e-5 absolute
+(the oracle recursion is fp64 like the kernel's); parameters as tests/test_gpu_parity.py.
+"""
+import numpy as np
+import pytest
+
+from oracle import ddrl_oracle as O
+from tests.gpu_harness import init_params, make_ctx
+
+pytestmark = pytest.mark.gpu
+N_ENVS, T = 4096, 200
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from ddrl_amd import build
+    build.build()
+
+
+@pytest.fixture(scope="module")
+def full():
+    import torch
+    from ddrl_amd.synthetic import SyntheticRollout
+    ctx, cfg, inst = make_ctx("QuantrupedMultiEnv_Local", N_ENVS, T)
+    params = init_params(ctx, cfg, 11, head_scale=1.0)
+    syn = SyntheticRollout(N_ENVS, T, cfg.obs_full_dim, cfg.n_agents, cfg.act_dim, "cuda:0", seed=5)
+    done = syn.dones_for_fragment()
+    ctx.observe(syn.obs[0])
+    ctx.rollout_fragment(syn.obs, syn.eps, syn.fw, syn.cfrc, done, syn.actions)
+    ctx.gae()
+    ctx.synchronize()
+    yield ctx, cfg, params, done.cpu().numpy()
+    ctx.close()
+
+
+def test_fullsize_records_match_oracle_rows(full):
+    ctx, cfg, params, _ = full
+    rng = np.random.default_rng(0)
+    for p in range(cfg.n_policies):
+        lay = ctx.layout[p]
+        rec = ctx.records_get(p)
+        assert rec.shape[0] == T * N_ENVS and np.isfinite(rec).all()
+        rows = rng.choice(rec.shape[0], 512, replace=False)
+        r = rec[rows]
+        d, A = cfg.obs_dim[p], cfg.act_dim
+        logits, value, _ = O.ffn_forward(params[p], r[:, :d])
+        np.testing.assert_allclose(r[:, lay["logit"]:lay["logit"] + 2 * A], logits, rtol=1e-5, atol=2e-5)
+        np.testing.assert_allclose(r[:, lay["vf"]], value, rtol=1e-5, atol=2e-5)
+        np.testing.assert_allclose(r[:, lay["logp"]], O.dg_logp(logits, r[:, lay["act"]:lay["act"] + A]),
+                                   rtol=1e-5, atol=2e-5)
+        # the normalized observation is clipped at +-10 (env-side MeanStdFilter)
+        assert np.abs(r[:, :d]).max() <= 10.0
+
+
+def test_fullsize_gae_chains_and_standardization(full):
+    ctx, cfg, params, done = full
+    rng = np.random.default_rng(1)
+    for p in range(cfg.n_policies):
+        lay = ctx.layout[p]
+        rec = ctx.records_get(p).reshape(T, N_ENVS, -1)          # Local: one slot per env
+        last_v = ctx.last_values_get(p)
+        chains = rng.choice(N_ENVS, 64, replace=False)
+        adv, vt = O.gae_fragment(rec[:, chains, lay["rew"]], rec[:, chains, lay["vf"]], done[:, chains].astype(bool),
+                                 last_v[chains], cfg.gamma, cfg.lambda_)
+        np.testing.assert_allclose(rec[:, chains, lay["adv"]], adv, rtol=1e-5, atol=2e-5)
+        np.testing.assert_allclose(rec[:, chains, lay["vt"]], vt, rtol=1e-5, atol=2e-5)
+        a = rec[:, :, lay["adv"]].reshape(-1).astype(np.float64)
+        mean, std = a.mean(), a.std()
+        an = ctx.adv_norm_get(p)
+        np.testing.assert_allclose(an, [mean, max(1e-4, std)], rtol=1e-5, atol=1e-6)
+
+
+def test_fullsize_first_step_and_stability(full):
+    import torch
+    ctx, cfg, params, _ = full
+    lay = ctx.layout[0]
+    R = T * N_ENVS
+    nb = R // 128
+    g = torch.Generator().manual_seed(3)
+    sh = torch.randperm(R, generator=g).to(torch.int32)
+    pe = torch.stack([torch.randperm(nb, generator=g) for _ in range(cfg.num_sgd_iter)]).to(torch.int32)
+    rec = ctx.records_get(0)
+    mean, den = ctx.adv_norm_get(0)
+    ctx.ppo_update(1, [sh.cuda(), None, None, None], [pe.cuda(), None, None, None], [0.2] * 4, max_steps=1)
+    ctx.synchronize()
+    d, A = cfg.obs_dim[0], cfg.act_dim
+    batch = dict(obs=rec[:, :d], actions=rec[:, lay["act"]:lay["act"] + A],
+                 logits=rec[:, lay["logit"]:lay["logit"] + 2 * A], logp=rec[:, lay["logp"]],
+                 vf_preds=rec[:, lay["vf"]], vt=rec[:, lay["vt"]],
+                 adv=((rec[:, lay["adv"]] - mean) / den).astype(np.float32))
+    shapes = O.ffn_param_shapes(d, 2 * A)
+    adam = O.Adam(sum(int(np.prod(s)) for _, s in shapes))
+    new, _ = O.ppo_update("ffn", params[0], shapes, adam, batch, sh.numpy(), pe.numpy(), np.float32(0.2), {},
+                          steps=1)
+    got = ctx.params_get(0)
+    want = O.pack(new, shapes)
+    diff = np.abs(got - want)
+    assert np.mean(diff <= 1e-5 + 1e-5 * np.abs(want)) >= 0.999, diff.max()
+    assert diff.max() <= 2 * cfg.lr + 1e-5
+    # 200 further steps (a new launch runs the schedule from its first minibatch again)
+    ctx.ppo_update(1, [sh.cuda(), None, None, None], [pe.cuda(), None, None, None], [0.2] * 4, max_steps=200)
+    ctx.synchronize()
+    assert np.isfinite(ctx.params_get(0)).all()
+    st = ctx.ppo_stats(0, 200)
+    assert np.isfinite(st).all()
