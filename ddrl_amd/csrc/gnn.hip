@@ -66,8 +66,8 @@ __device__ __forceinline__ float quad_next(float v) { return dpp_mov<0x39>(v); }
 #define L_DOUT (L_HP + 256)
 #define L_ST (L_DOUT + 16)
 #define L_SEL (L_ST + 32)
-#define L_TP (L_SEL + 8)          // per-wave 4 x 16x16 transpose tiles of the hypernet backward
-#define L_QT (L_TP + 4 * 1024)    // quaternions of the tile's 16 graph-nodes [16][4]
+#define L_TP (L_SEL + 8)          // per-wave 2 x 4 x 16x16 transpose tiles of the hypernet backward
+#define L_QT (L_TP + 8 * 1024)    // quaternions of the tile's 16 graph-nodes [16][4]
 #define L_TOTAL (L_QT + 64)
 
 template <int A, int MODE, int NET>
@@ -409,11 +409,11 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
   float qb[4];
 #pragma unroll
   for (int s4 = 0; s4 < 4; ++s4) qb[s4] = c < 4 ? qt[(4 * s4 + q) * 4 + c] : (c == 4 ? 1.f : 0.f);
-  float* tp = lds + L_TP + 1024 * w;   // one 16x16 tile per column block t
-#pragma unroll
-  for (int k = 0; k < GNI; ++k) {
-    const int i = w + 4 * k;
-    if (i >= GF) break;
+  // Software-pipelined over the feature rows i of this wave: the dpre tiles of row k + 1 are
+  // computed (MFMA, tanh: VALU) and stored to the other half of a double-buffered LDS tile
+  // while the 16 weight-gradient MFMAs of row k run on operands already in registers.
+  float* tpb = lds + L_TP + 2048 * w;   // [2][4 column blocks][16 x 16]
+  auto dpre_tiles = [&](int k, float* tp) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const floatx4 pre = mfma4(we[k][t], qv, be[k][t]);
@@ -425,13 +425,28 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
       }
       *reinterpret_cast<floatx4*>(tp + 256 * t + c * 16 + 4 * q) = dp;   // [row c][j 4q + r]
     }
+  };
+  constexpr int NK = (GF + 3) / 4;   // feature rows of wave 0 (waves 1..3 have NK or NK - 1)
+  static_assert(NK == GNI, "feature rows per wave");
+  dpre_tiles(0, tpb);
+#pragma unroll
+  for (int k = 0; k < GNI; ++k) {
+    const int i = w + 4 * k;
+    if (i >= GF) break;
+    const float* tp = tpb + 1024 * (k & 1);
+    float a[4][4];
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) a[s4][t] = tp[256 * t + (4 * s4 + q) * 16 + c];
+    if (k + 1 < GNI && i + 4 < GF) dpre_tiles(k + 1, tpb + 1024 * ((k + 1) & 1));
     floatx4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[t] = splat4(0.f);
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = mfma4(tp[256 * t + (4 * s4 + q) * 16 + c], qb[s4], acc[t]);
+      for (int t = 0; t < 4; ++t) acc[t] = mfma4(a[s4][t], qb[s4], acc[t]);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int j = i * 64 + 16 * t + 4 * q;                  // acc[r]: column j + r, qd = c
