@@ -478,16 +478,17 @@ __device__ __forceinline__ float gnn_stage_load(const GnnArgs& ga, int step, int
 __global__ void __launch_bounds__(256) k_gnn_reduce(GnnArgs ga, int ntiles, int n) {
   __shared__ float red[4];
   const int p = blockIdx.x * 256 + threadIdx.x;
-  // the next step's records -> stage (this step's gradient kernel has finished reading it);
-  // the loads overlap the partial-gradient loads below
-  int sdst = -1;
-  const float sv_next = ga.stage_next ? gnn_stage_load(ga, ga.step + 1, p, sdst) : 0.f;
   // all tile partials of this parameter in flight at once (a runtime-bound loop would wait
   // for each load before the next add), then summed in tile order
   float v[DDRL_MB / 4];
 #pragma unroll
   for (int t = 0; t < DDRL_MB / 4; ++t)
     v[t] = (p < n && t < ntiles) ? ga.part[(size_t)t * ga.part_stride + p] : 0.f;
+  // the next step's records -> stage (this step's gradient kernel has finished reading it);
+  // issued after the partial loads, so its dependent row-table -> record chain waits behind
+  // them instead of holding them back
+  int sdst = -1;
+  const float sv_next = ga.stage_next ? gnn_stage_load(ga, ga.step + 1, p, sdst) : 0.f;
   float s = 0.f;
 #pragma unroll
   for (int t = 0; t < DDRL_MB / 4; ++t) s += v[t];
@@ -540,6 +541,7 @@ __global__ void __launch_bounds__(256) k_gnn_adam(GnnArgs ga, int nred, int n) {
   const float g0 = pv ? ga.grad[p] : 0.f;
   float mi = pv ? U.m[p] : 0.f, vi = pv ? U.v[p] : 0.f;
   const float th0 = pv ? U.theta[p] : 0.f;
+  const float b1p = ga.bp_cur[0], b2p = ga.bp_cur[1];
   if (threadIdx.x < 64) {
     // squared-norm partials of the reduction blocks: the same butterfly in every block
     float part = 0.f;
@@ -553,14 +555,13 @@ __global__ void __launch_bounds__(256) k_gnn_adam(GnnArgs ga, int nred, int n) {
         U.stats[(size_t)ga.step * 8 + 6] = gn;
         U.stats[(size_t)ga.step * 8 + 7] = scale_s;
       }
-      U.beta_pow[0] = ga.bp_cur[0] * h.b1;
-      U.beta_pow[1] = ga.bp_cur[1] * h.b2;
+      U.beta_pow[0] = b1p * h.b1;
+      U.beta_pow[1] = b2p * h.b2;
     }
   }
 done:
   __syncthreads();
   if (!pv) return;
-  const float b1p = ga.bp_cur[0], b2p = ga.bp_cur[1];
   const float alpha = h.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   const float g = g0 * scale_s;
   mi = mi + (g - mi) * (1.f - h.b1);
