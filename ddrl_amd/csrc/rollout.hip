@@ -238,14 +238,15 @@ void launch_observe_gnn(hipStream_t s, const RouteArgs& ra, const float* obs, co
 }
 
 // ------------------------------------------------------------------------------------
-// a4 + a6 + a7: fused rollout forward.  Workgroup = 4 waves = 64 rows of ONE policy
+// a4 + a6 + a7: fused rollout forward.  Workgroup = 8 waves = 64 rows of ONE policy
 // (grid.y = policy).  The policy's weights are staged once into LDS in the swizzled
-// image; each wave runs both branches for its 16 rows from registers (MFMA 16x16x4 f32),
-// samples a = mean + exp(log_std) * eps, computes logp, writes the training record and
-// scatters clip(a, -1, 1) into the env action vector.
+// image; waves 0-3 run the policy branch and waves 4-7 the value branch of the same four
+// 16-row tiles, from registers (MFMA 16x16x4 f32), so the two branch chains run side by side
+// on each SIMD.  The policy waves sample a = mean + exp(log_std) * eps, compute logp, write
+// the training record and scatter clip(a, -1, 1) into the env action vector.
 // ------------------------------------------------------------------------------------
 template <int A, int KS1>
-__global__ void __launch_bounds__(256) k_act_ffn(RouteArgs ra, ActArgs aa) {
+__global__ void __launch_bounds__(512) k_act_ffn(RouteArgs ra, ActArgs aa) {
   constexpr int O = 2 * A;
   extern __shared__ float lds[];
   const int p = blockIdx.y;
@@ -255,11 +256,13 @@ __global__ void __launch_bounds__(256) k_act_ffn(RouteArgs ra, ActArgs aa) {
   if (row0 >= C) return;
   const int d = pr.d;
   NetLds PW, VW;
-  stage_weights(aa.theta[p], d, A, lds, PW, VW, 256);
+  stage_weights(aa.theta[p], d, A, lds, PW, VW, 512);
   __syncthreads();
 
   const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4, w = threadIdx.x >> 6;
-  const int row = row0 + 16 * w + c;
+  const bool value_wave = w >= 4;
+  if (aa.bootstrap && !value_wave) return;   // bootstrap: V(s_T) only
+  const int row = row0 + 16 * (w & 3) + c;
   const bool valid = row < C;
   const float* xs = aa.stage[p] + (size_t)(valid ? row : 0) * d;
   float xop[12];
@@ -269,11 +272,14 @@ __global__ void __launch_bounds__(256) k_act_ffn(RouteArgs ra, ActArgs aa) {
     xop[s] = (s < KS1 && f < d && valid) ? xs[f] : 0.f;
   }
   floatx4 h1[4], h2[4];
-  float vout[1];
-  ffn_branch_fwd<1, KS1>(VW, xop, h1, h2, vout);
   const RecLayout& L = aa.lay[p];
-  if (aa.bootstrap) {
-    if (valid && q == 0) aa.last_v[p][row] = vout[0];
+  if (value_wave) {
+    float vout[1];
+    ffn_branch_fwd<1, KS1>(VW, xop, h1, h2, vout);
+    if (valid && q == 0) {
+      if (aa.bootstrap) aa.last_v[p][row] = vout[0];
+      else aa.rec[p][((size_t)aa.t * C + row) * L.stride + L.vf] = vout[0];
+    }
     return;
   }
   float logits[O];
@@ -315,14 +321,13 @@ __global__ void __launch_bounds__(256) k_act_ffn(RouteArgs ra, ActArgs aa) {
     for (int j = 0; j < O; ++j) rp[L.logit + j] = logits[j];
   } else if (q == 2) {
     rp[L.logp] = logp;
-    rp[L.vf] = vout[0];
     if (L.cid >= 0) rp[L.cid] = (float)slot;
   }
 }
 
 template <int A, int KS1>
 static void launch_act_t(hipStream_t s, dim3 grid, const RouteArgs& ra, const ActArgs& aa) {
-  hipLaunchKernelGGL((k_act_ffn<A, KS1>), grid, dim3(256), LDS_WEIGHTS_FLOATS(2 * A) * 4, s, ra, aa);
+  hipLaunchKernelGGL((k_act_ffn<A, KS1>), grid, dim3(512), LDS_WEIGHTS_FLOATS(2 * A) * 4, s, ra, aa);
 }
 
 void launch_act_ffn(hipStream_t s, const RouteArgs& ra, const ActArgs& aa) {
