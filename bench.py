@@ -147,11 +147,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # DDRL_DIST_BACKEND=gloo rehearses the multi-rank path on one GPU (ranks share device 0,
+    # the end-of-run reductions go over gloo on the host); the default is RCCL ("nccl")
+    backend = os.environ.get("DDRL_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     from ddrl_amd import native as N
     from ddrl_amd.build import build
@@ -188,7 +196,7 @@ def main():
     upd_ms = []
     if ddp:
         from ddrl_amd.ddp import Comm, DataParallelLearner, HipBackend, sync_filters, sync_standardize
-        comm = Comm(f"cuda:{local}")
+        comm = Comm(f"cuda:{local}" if backend == "nccl" else "cpu")
         learner = DataParallelLearner(HipBackend(ctx), comm, 0, 128, args.ddp_mode)
         filter_base = ctx.filter_get()
         ctx.filter_delta_reset()
@@ -289,10 +297,11 @@ def main():
     t_max = elapsed
     env_steps = T * n_local * args.steps
     if dist is not None:
-        tt = torch.tensor([elapsed], device="cuda")
+        red_dev = "cuda" if backend == "nccl" else "cpu"
+        tt = torch.tensor([elapsed], device=red_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt.item())
-        es = torch.tensor([env_steps], device="cuda", dtype=torch.float64)
+        es = torch.tensor([env_steps], device=red_dev, dtype=torch.float64)
         dist.all_reduce(es)
         env_steps = int(es.item())
 
