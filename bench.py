@@ -153,8 +153,11 @@ def main():
     if backend != "nccl":
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
+    # DDRL_FORCE_DDP=1 runs the data-parallel learner even at one rank (torchrun, world 1):
+    # the RCCL path of the shared-policy configurations exercised on a one-GPU box
+    force_ddp = os.environ.get("DDRL_FORCE_DDP") == "1"
     dist = None
-    if world > 1:
+    if world > 1 or force_ddp:
         import torch.distributed as dist
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -179,7 +182,7 @@ def main():
     gnn = cfg.model_kind == N.MODEL_GNN
     # shared-policy envs on several GPUs train data-parallel (identical weights on every
     # rank); independent-policy envs are replicas (own weights per rank)
-    ddp = world > 1 and P == 1
+    ddp = (world > 1 or force_ddp) and P == 1
     rng = np.random.default_rng(1234 if ddp else 1234 + rank)
     from ddrl_amd.trainer import glorot_ffn_flat
     from ddrl_amd.models import glorot_gnn_flat
@@ -195,9 +198,15 @@ def main():
     ev_upd = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     upd_ms = []
     if ddp:
-        from ddrl_amd.ddp import Comm, DataParallelLearner, HipBackend, sync_filters, sync_standardize
+        from ddrl_amd.ddp import (Comm, DataParallelLearner, HipBackend, NativeDataParallelLearner,
+                                  native_comm_init, sync_filters, sync_standardize)
         comm = Comm(f"cuda:{local}" if backend == "nccl" else "cpu")
-        learner = DataParallelLearner(HipBackend(ctx), comm, 0, 128, args.ddp_mode)
+        if backend == "nccl" and os.environ.get("DDRL_DDP_LOOP", "native") == "native":
+            # the minibatch loop inside the library on its own RCCL communicator
+            native_comm_init(ctx, comm)
+            learner = NativeDataParallelLearner(ctx, comm, 0, 128, args.ddp_mode)
+        else:
+            learner = DataParallelLearner(HipBackend(ctx), comm, 0, 128, args.ddp_mode)
         filter_base = ctx.filter_get()
         ctx.filter_delta_reset()
         grad = torch.zeros(ctx.n_params[0], dtype=torch.float32, device=f"cuda:{local}")

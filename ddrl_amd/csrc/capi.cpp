@@ -9,6 +9,8 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "../../include/ddrl_hip.h"
 #include "kernels.h"
 
@@ -25,6 +27,12 @@ int fail(const std::string& msg) {
     hipError_t e_ = (x);                                                            \
     if (e_ != hipSuccess)                                                           \
       return fail(std::string(#x) + ": " + hipGetErrorString(e_));                  \
+  } while (0)
+
+#define NCCLCHK(x)                                                                  \
+  do {                                                                              \
+    ncclResult_t r_ = (x);                                                          \
+    if (r_ != ncclSuccess) return fail(std::string(#x) + ": " + ncclGetErrorString(r_)); \
   } while (0)
 
 #define CHK_CTX(c) \
@@ -67,6 +75,9 @@ struct ddrl_ctx {
   GnnScratch gnn{};               // GraphNet step scratch (per-tile partial gradients, ...)
   // host-variant staging
   float *h_obs = nullptr, *h_eps = nullptr, *h_act = nullptr;
+  ncclComm_t comm = nullptr;           // data-parallel learner (ddrl_comm_init)
+  UpdateArgs* d_ddp = nullptr;         // per-step arguments of ddrl_ppo_update_ddp
+  size_t ddp_cap = 0;
   float *h_fw = nullptr, *h_cfrc = nullptr;
   uint8_t* h_done = nullptr;
   std::vector<void*> allocs;
@@ -242,6 +253,8 @@ int ddrl_ctx_destroy(ddrl_ctx* c) {
   if (!c) return 0;
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  if (c->d_ddp) (void)hipFree(c->d_ddp);
   for (void* p : c->allocs) (void)hipFree(p);
   delete c;
   return 0;
@@ -670,6 +683,85 @@ int ddrl_ppo_apply(ddrl_ctx* c, int pid, const float* grad) {
   launch_apply_adam(c->stream, grad, P.n_params, P.theta, P.m, P.v, P.beta_pow, make_hyper(c, 1));
   HIPCHK(hipGetLastError());
   return 0;
+}
+
+static_assert(sizeof(ncclUniqueId) == DDRL_COMM_ID_BYTES, "RCCL unique id size");
+
+int ddrl_comm_unique_id(void* out, size_t n) {
+  if (!out || n < sizeof(ncclUniqueId)) return fail("unique id buffer too small");
+  ncclUniqueId id;
+  NCCLCHK(ncclGetUniqueId(&id));
+  std::memcpy(out, &id, sizeof(id));
+  return 0;
+}
+
+int ddrl_comm_init(ddrl_ctx* c, const void* id, int rank, int nranks) {
+  CHK_CTX(c);
+  if (!id || nranks < 1 || rank < 0 || rank >= nranks) return fail("bad communicator arguments");
+  if (c->comm) return fail("the context already has a communicator");
+  HIPCHK(hipSetDevice(c->device));
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof(uid));
+  NCCLCHK(ncclCommInitRank(&c->comm, nranks, uid, rank));
+  return 0;
+}
+
+int ddrl_comm_allreduce(ddrl_ctx* c, float* buf, size_t n) {
+  CHK_CTX(c);
+  if (!c->comm) return fail("no communicator (ddrl_comm_init)");
+  if (!buf) return fail("null buffer");
+  NCCLCHK(ncclAllReduce(buf, buf, n, ncclFloat32, ncclSum, c->comm, c->stream));
+  return 0;
+}
+
+int ddrl_ppo_update_ddp(ddrl_ctx* c, int pid, const int32_t* shuffle, const int32_t* perm, int E, int nb,
+                        int m, float kl, float gscale) {
+  CHK_CTX(c);
+  if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
+  if (!c->comm) return fail("no communicator (ddrl_comm_init)");
+  if (!shuffle || !perm || E < 1 || nb < 1) return fail("bad schedule");
+  if (m < 1 || m > 128) return fail("rows_per_rank must be in [1, 128]");
+  if (nb > c->cfg.num_sgd_iter * c->pol[pid].nb) return fail("more minibatches than the stats buffer holds");
+  Policy& P = c->pol[pid];
+  const int steps = E * nb;
+  const UpdateHyper h = make_hyper(c, 1);
+  const float inv_n = 1.f / c->cfg.sgd_minibatch_size;
+  std::vector<UpdateArgs> ua((size_t)steps);
+  for (int e = 0; e < E; ++e)
+    for (int b = 0; b < nb; ++b) {
+      const int slot = perm[(size_t)e * nb + b];
+      if (slot < 0 || (size_t)(slot + 1) * m > (size_t)P.R) return fail("minibatch slot out of range");
+      UpdateArgs u = make_update(c, pid, shuffle + (size_t)slot * m, c->zero_perm, kl);
+      u.nb = 1; u.n_epochs = 1; u.max_steps = 1; u.step0 = 0; u.grad_out = P.grad;
+      u.stats = e == E - 1 ? P.stats + (size_t)b * 8 : nullptr;
+      ua[(size_t)e * nb + b] = u;
+    }
+  const bool ffn = c->cfg.model_kind == DDRL_MODEL_FFN;
+  if (ffn) {   // the fused kernel reads its arguments from device memory: all steps at once
+    if (c->ddp_cap < (size_t)steps) {
+      if (c->d_ddp) HIPCHK(hipFree(c->d_ddp));
+      c->d_ddp = nullptr;
+      c->ddp_cap = 0;
+      HIPCHK(hipMalloc(&c->d_ddp, sizeof(UpdateArgs) * (size_t)steps));
+      c->ddp_cap = steps;
+    }
+    HIPCHK(hipMemcpyAsync(c->d_ddp, ua.data(), sizeof(UpdateArgs) * (size_t)steps, hipMemcpyHostToDevice, c->stream));
+  }
+  c->kl_last[pid] = kl;
+  for (int s = 0; s < steps; ++s) {
+    if (ffn)
+      launch_update_ffn(c->stream, c->d_ddp + s, h, m, inv_n, c->cfg.act_dim, P.d, P.lay.stride, c->cfg.leg_coupling,
+                        c->xchg, c->gx, 1, c->err);
+    else
+      launch_step_gnn(c->stream, ua[s], h, 0, m, inv_n, c->gnn);
+    NCCLCHK(ncclAllReduce(P.grad, P.grad, (size_t)P.n_params, ncclFloat32, ncclSum, c->comm, c->stream));
+    launch_apply_adam(c->stream, P.grad, P.n_params, P.theta, P.m, P.v, P.beta_pow, h, gscale);
+  }
+  HIPCHK(hipGetLastError());
+  // the pageable argument copy must not outlive ua (hipMemcpyAsync from pageable memory is
+  // staged before it returns on ROCm, but synchronize to be independent of that)
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return check_err(c);
 }
 
 int ddrl_policy_forward(ddrl_ctx* c, int pid, const float* obs, const int32_t* node, int n,

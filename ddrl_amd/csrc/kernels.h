@@ -133,8 +133,9 @@ void launch_update_ffn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHype
                        int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp, int* err);
 size_t gx_bytes(int P);
 // clip_by_global_norm + tf1 Adam on a flat (all-reduced) gradient vector
+// gscale multiplies the gradient before the clip (1 / ranks in the "local" data-parallel mode)
 void launch_apply_adam(hipStream_t s, const float* grad, int n, float* theta, float* m, float* v,
-                       float* beta_pow, const UpdateHyper& h);
+                       float* beta_pow, const UpdateHyper& h, float gscale = 1.f);
 
 // ---- ModelV2.forward / value_function on arbitrary rows ----
 struct ForwardArgs {

@@ -893,11 +893,14 @@ size_t gx_bytes(int P) { return sizeof(unsigned long long) * (size_t)P * 2 * 2 *
 // ------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(1024) k_apply_adam(const float* __restrict__ grad, int n,
                                                      float* theta, float* m, float* v,
-                                                     float* beta_pow, UpdateHyper h) {
+                                                     float* beta_pow, UpdateHyper h, float gscale) {
   __shared__ float red[16];
   const int tid = threadIdx.x;
   float ss = 0.f;
-  for (int i = tid; i < n; i += 1024) ss += grad[i] * grad[i];
+  for (int i = tid; i < n; i += 1024) {
+    const float gi = grad[i] * gscale;   // gscale: 1 / ranks of the "local" data-parallel mode
+    ss += gi * gi;
+  }
   ss = wave_sum(ss);
   if ((tid & 63) == 0) red[tid >> 6] = ss;
   __syncthreads();
@@ -913,7 +916,7 @@ __global__ void __launch_bounds__(1024) k_apply_adam(const float* __restrict__ g
   const float alpha = h.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   const float c1 = 1.f - h.b1, c2 = 1.f - h.b2;
   for (int i = tid; i < n; i += 1024) {
-    const float g = grad[i] * scale;
+    const float g = (grad[i] * gscale) * scale;
     float mi = m[i], vi = v[i];
     mi = mi + (g - mi) * c1;
     vi = vi + (g * g - vi) * c2;
@@ -929,6 +932,6 @@ __global__ void __launch_bounds__(1024) k_apply_adam(const float* __restrict__ g
 }
 
 void launch_apply_adam(hipStream_t s, const float* grad, int n, float* theta, float* m, float* v,
-                       float* beta_pow, const UpdateHyper& h) {
-  hipLaunchKernelGGL(k_apply_adam, dim3(1), dim3(1024), 0, s, grad, n, theta, m, v, beta_pow, h);
+                       float* beta_pow, const UpdateHyper& h, float gscale) {
+  hipLaunchKernelGGL(k_apply_adam, dim3(1), dim3(1024), 0, s, grad, n, theta, m, v, beta_pow, h, gscale);
 }

@@ -21,7 +21,10 @@ Per iteration (RLlib semantics restated for G ranks that each own N / G envs):
 Independent-policy configurations (Local, C3) need none of this: every rank is a replica.
 
 The learner drives a backend with grad / apply / stats (`HipBackend` wraps the C-ABI
-context); the collectives go through torch.distributed.
+context); the collectives go through torch.distributed.  On RCCL the whole minibatch loop
+can instead run inside the library (`NativeDataParallelLearner`: the context's own RCCL
+communicator from `ddrl_comm_init`, `ddrl_ppo_update_ddp` enqueues grad -> ncclAllReduce ->
+Adam per step with no Python between them).
 """
 from __future__ import annotations
 
@@ -110,6 +113,17 @@ class HipBackend:
         return self.ctx.ppo_stats(pid, n)
 
 
+def native_comm_init(ctx, comm):
+    """Give the C-ABI context its own RCCL communicator over the ranks of `comm`: rank 0 makes
+    the unique id, a torch.distributed broadcast hands it to the others."""
+    from . import native
+    uid = native.comm_unique_id() if comm.rank == 0 else bytes(native.COMM_ID_BYTES)
+    t = comm.torch.tensor(list(uid), dtype=comm.torch.uint8, device=comm.device)
+    if comm.world > 1:
+        comm.dist.broadcast(t, src=0, group=comm.group)
+    ctx.comm_init(bytes(t.cpu().tolist()), comm.rank, comm.world)
+
+
 class DataParallelLearner:
     def __init__(self, backend, comm, pid=0, minibatch=128, mode="split"):
         if mode not in ("split", "local"):
@@ -146,6 +160,25 @@ class DataParallelLearner:
                 if self.grad_scale != 1.0:
                     grad.mul_(self.grad_scale)
                 self.backend.apply(self.pid, grad)
+        return self._kl(nb)
+
+    def _kl(self, nb):
         st = self.backend.stats(self.pid, nb)
         kl_local = float(np.mean(st[:, 3].astype(np.float64)))
         return float(self.comm.all_reduce_np(np.array([kl_local]))[0]) / self.comm.world
+
+
+class NativeDataParallelLearner(DataParallelLearner):
+    """DataParallelLearner whose per-step loop runs inside the library: ddrl_ppo_update_ddp
+    enqueues gradient -> RCCL all-reduce -> Adam for every minibatch from C++, on the
+    context's stream and communicator (`native_comm_init`), the same arithmetic in the same
+    order as `learn` above (which it is tested against bit for bit)."""
+
+    def __init__(self, ctx, comm, pid=0, minibatch=128, mode="split"):
+        super().__init__(HipBackend(ctx), comm, pid, minibatch, mode)
+        self.ctx = ctx
+
+    def learn(self, shuffle, perms, kl_coeff, grad=None):
+        perms = np.asarray(perms, np.int32)
+        self.ctx.ppo_update_ddp(self.pid, shuffle, perms, self.rows_per_rank, kl_coeff, self.grad_scale)
+        return self._kl(perms.shape[1])

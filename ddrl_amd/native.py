@@ -79,6 +79,10 @@ _SIGS = {
     "ddrl_ppo_stats": ([VP, C.c_int, VP, C.c_size_t], C.c_int),
     "ddrl_ppo_grad": ([VP, C.c_int, VP, C.c_int, f32, VP, C.c_int], C.c_int),
     "ddrl_ppo_apply": ([VP, C.c_int, VP], C.c_int),
+    "ddrl_comm_unique_id": ([VP, C.c_size_t], C.c_int),
+    "ddrl_comm_init": ([VP, VP, C.c_int, C.c_int], C.c_int),
+    "ddrl_comm_allreduce": ([VP, VP, C.c_size_t], C.c_int),
+    "ddrl_ppo_update_ddp": ([VP, C.c_int, VP, VP, C.c_int, C.c_int, C.c_int, f32, f32], C.c_int),
     "ddrl_policy_forward": ([VP, C.c_int, VP, VP, C.c_int, VP, VP], C.c_int),
     "ddrl_device_buffers": ([VP, C.c_int, C.POINTER(VP), C.POINTER(VP), C.POINTER(VP), C.POINTER(VP)], C.c_int),
     "ddrl_records_get": ([VP, C.c_int, VP, C.c_size_t], C.c_int),
@@ -104,6 +108,14 @@ def header_symbols(path=HEADER):
 
 
 ABI_VERSION = 3   # DDRL_ABI_VERSION of include/ddrl_hip.h (ddrl_cfg layout, record layout)
+COMM_ID_BYTES = 128   # DDRL_COMM_ID_BYTES (sizeof ncclUniqueId)
+
+
+def comm_unique_id():
+    """A fresh RCCL unique id (rank 0 makes it, the caller hands it to the other ranks)."""
+    buf = (C.c_uint8 * COMM_ID_BYTES)()
+    _ck(load().ddrl_comm_unique_id(buf, COMM_ID_BYTES))
+    return bytes(buf)
 
 
 def load(path: str = LIB_PATH):
@@ -335,6 +347,21 @@ class Context:
 
     def ppo_apply(self, pid, grad_dev):
         _ck(self.lib.ddrl_ppo_apply(self.h, pid, _ptr(grad_dev)))
+
+    def comm_init(self, unique_id, rank, nranks):
+        """Join the RCCL communicator named by `unique_id` (bytes from comm_unique_id())."""
+        buf = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(bytes(unique_id))
+        _ck(self.lib.ddrl_comm_init(self.h, buf, rank, nranks))
+
+    def comm_allreduce(self, buf_dev):
+        _ck(self.lib.ddrl_comm_allreduce(self.h, _ptr(buf_dev), buf_dev.numel()))
+
+    def ppo_update_ddp(self, pid, shuffle_dev, perms, rows_per_rank, kl_coeff, grad_scale):
+        """The data-parallel minibatch loop in C++ (gradient -> RCCL all-reduce -> Adam per step)."""
+        perms = np.ascontiguousarray(perms, np.int32)
+        E, nb = perms.shape
+        _ck(self.lib.ddrl_ppo_update_ddp(self.h, pid, _ptr(shuffle_dev), perms.ctypes.data, E, nb,
+                                         rows_per_rank, kl_coeff, grad_scale))
 
     def policy_forward(self, pid, obs_dev, n, logits_dev, values_dev, node_dev=None):
         _ck(self.lib.ddrl_policy_forward(self.h, pid, _ptr(obs_dev), _ptr(node_dev), n,

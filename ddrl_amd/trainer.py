@@ -94,10 +94,16 @@ class PPOTrainer:
         self.iteration = 0
         self.parallel = c.get("parallel") or ("ddp" if self.world > 1 and P == 1 else "replicas")
         if self.parallel == "ddp":
-            from .ddp import Comm, DataParallelLearner, HipBackend
-            self.comm = Comm(self.device if dist.get_backend() == "nccl" else "cpu")
-            self.learner = DataParallelLearner(HipBackend(self.ctx), self.comm, 0, self.cfg.sgd_minibatch_size,
-                                               c.get("ddp_mode", "split"))
+            from .ddp import Comm, DataParallelLearner, HipBackend, NativeDataParallelLearner, native_comm_init
+            rccl = dist.get_backend() == "nccl"
+            self.comm = Comm(self.device if rccl else "cpu")
+            if rccl and c.get("ddp_loop", "native") == "native":
+                native_comm_init(self.ctx, self.comm)
+                self.learner = NativeDataParallelLearner(self.ctx, self.comm, 0, self.cfg.sgd_minibatch_size,
+                                                         c.get("ddp_mode", "split"))
+            else:
+                self.learner = DataParallelLearner(HipBackend(self.ctx), self.comm, 0, self.cfg.sgd_minibatch_size,
+                                                   c.get("ddp_mode", "split"))
             self.filter_base = self.ctx.filter_get()
             self.ctx.filter_delta_reset()
             self.pfilter_base = ([self.ctx.policy_filter_get(p) for p in range(P)]

@@ -187,6 +187,23 @@ int ddrl_ppo_grad(ddrl_ctx* ctx, int pid, const int32_t* rows_dev, int n_rows,
                   float kl_coeff, float* grad_dev, int stats_step);
 int ddrl_ppo_apply(ddrl_ctx* ctx, int pid, const float* grad_dev);
 
+/* RCCL communicator of a data-parallel learner (SURVEY 8(b) "ddrl_comm_init"): rank 0 makes
+ * the unique id (DDRL_COMM_ID_BYTES bytes, handed to the other ranks by the caller, e.g. a
+ * torch.distributed broadcast), every rank joins with its rank; one communicator per context,
+ * on the context's device.  comm_allreduce sums n floats in place on the context's stream. */
+#define DDRL_COMM_ID_BYTES 128
+int ddrl_comm_unique_id(void* id_out, size_t n);
+int ddrl_comm_init(ddrl_ctx* ctx, const void* id, int rank, int nranks);
+int ddrl_comm_allreduce(ddrl_ctx* ctx, float* buf_dev, size_t n);
+/* The data-parallel minibatch SGD of policy pid, enqueued from C++ on the context's stream
+ * (per step: gradient of this rank's rows -> RCCL all-reduce -> clip + Adam), the per-step
+ * loop of ddrl_amd/ddp.py DataParallelLearner.learn without a host round trip per call.
+ *   shuffle_dev: this rank's row permutation; perm_host[n_epochs][nb]: minibatch slots;
+ *   rows_per_rank: 128 / ranks ("split") or 128 ("local"); grad_scale: 1 or 1 / ranks.
+ * Learner statistics of the last epoch land in ddrl_ppo_stats rows 0 .. nb - 1. */
+int ddrl_ppo_update_ddp(ddrl_ctx* ctx, int pid, const int32_t* shuffle_dev, const int32_t* perm_host,
+                        int n_epochs, int nb, int rows_per_rank, float kl_coeff, float grad_scale);
+
 /* Model forward (ModelV2.forward + value_function) on arbitrary rows:
  * obs_dev[n][d] (ffn; + node_dev[n] = leg index with leg_coupling) or X_dev[n][4][23] +
  * node_dev[n] (gnn). */
