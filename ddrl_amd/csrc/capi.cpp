@@ -69,6 +69,7 @@ struct ddrl_ctx {
   UpdateArgs* d_uargs = nullptr;  // device copy of the per-workgroup update arguments
   unsigned long long* xchg = nullptr;  // norm^2 exchange granules of the update kernel
   unsigned long long* gx = nullptr;    // partial-gradient granules of the row-split update
+  unsigned upd_epoch = 0;              // update launches so far (granule tag epochs)
   int update_split = 2;                // workgroups per branch of the fused update (1 or 2)
   int* err = nullptr;                  // device error word (exchange timeout)
   float kl_last[DDRL_MAXP] = {0};
@@ -202,13 +203,14 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
     }
     const size_t stage_n = g.model_kind == DDRL_MODEL_GNN ? (size_t)N * 4 * 23 : (size_t)P.C * P.d;
     rc = rc || dalloc(c, &P.theta, P.n_params) || dalloc(c, &P.m, P.n_params) ||
-         dalloc(c, &P.v, P.n_params) || dalloc(c, &P.beta_pow, 2) || dalloc(c, &P.grad, P.n_params) ||
+         dalloc(c, &P.v, P.n_params) || dalloc(c, &P.beta_pow, 4) || dalloc(c, &P.grad, P.n_params) ||
          dalloc(c, &P.rec, (size_t)P.R * P.lay.stride) || dalloc(c, &P.stage, stage_n) ||
          dalloc(c, &P.last_v, P.C) || dalloc(c, &P.adv_norm, 2) ||
          dalloc(c, &P.partials, 2 * (size_t)((P.C + 255) / 256) + 4) ||
          dalloc(c, &P.stats, (size_t)g.num_sgd_iter * P.nb * 8);
     if (!rc) {
-      float bp[2] = {g.adam_beta1, g.adam_beta2};
+      // beta1^t, beta2^t, then the arrival counter of the multi-workgroup apply kernel (0)
+      float bp[4] = {g.adam_beta1, g.adam_beta2, 0.f, 0.f};
       if (hipMemcpy(P.beta_pow, bp, sizeof(bp), hipMemcpyHostToDevice) != hipSuccess) rc = fail("init beta_pow");
       float an[2] = {0.f, 1.f};
       if (hipMemcpy(P.adv_norm, an, sizeof(an), hipMemcpyHostToDevice) != hipSuccess) rc = fail("init adv_norm");
@@ -622,7 +624,7 @@ int ddrl_ppo_update(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const 
   HIPCHK(hipMemcpyAsync(c->d_uargs, ua, sizeof(UpdateArgs) * n, hipMemcpyHostToDevice, c->stream));
   if (c->cfg.model_kind == DDRL_MODEL_FFN)
     launch_update_ffn(c->stream, c->d_uargs, h, 128, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim, maxd, maxs,
-                      c->cfg.leg_coupling, c->xchg, c->gx, c->update_split, c->err);
+                      c->cfg.leg_coupling, c->xchg, c->gx, c->update_split, c->err, &c->upd_epoch);
   else if (c->pol[0].last_steps > 0) {   // one shared policy
     const int last = c->pol[0].last_steps;
     launch_gnn_schedule(c->stream, ua[0], last, 0, c->gnn);
@@ -653,6 +655,11 @@ int ddrl_ppo_stats(ddrl_ctx* c, int pid, float* host, size_t n_steps) {
   return 0;
 }
 
+// Workgroups per branch of a gradient-only update launch: the row split of the fused update
+// when the rows fill both halves (64 each), else one.  ddrl_ppo_grad and ddrl_ppo_update_ddp
+// share this rule, so the two data-parallel loops run the same kernels.
+static int grad_split(const ddrl_ctx* c, int n_rows) { return n_rows > 64 ? c->update_split : 1; }
+
 int ddrl_ppo_grad(ddrl_ctx* c, int pid, const int32_t* rows, int n_rows, float kl, float* grad,
                   int stats_step) {
   CHK_CTX(c);
@@ -668,7 +675,8 @@ int ddrl_ppo_grad(ddrl_ctx* c, int pid, const int32_t* rows, int n_rows, float k
   HIPCHK(hipMemcpyAsync(c->d_uargs, &u, sizeof(UpdateArgs), hipMemcpyHostToDevice, c->stream));
   if (c->cfg.model_kind == DDRL_MODEL_FFN)
     launch_update_ffn(c->stream, c->d_uargs, h, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim,
-                      c->pol[pid].d, c->pol[pid].lay.stride, c->cfg.leg_coupling, c->xchg, c->gx, 1, c->err);
+                      c->pol[pid].d, c->pol[pid].lay.stride, c->cfg.leg_coupling, c->xchg, c->gx,
+                      grad_split(c, n_rows), c->err, &c->upd_epoch);
   else
     launch_step_gnn(c->stream, u, h, 0, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->gnn);
   HIPCHK(hipGetLastError());
@@ -680,7 +688,7 @@ int ddrl_ppo_apply(ddrl_ctx* c, int pid, const float* grad) {
   if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
   if (!grad) return fail("null grad");
   Policy& P = c->pol[pid];
-  launch_apply_adam(c->stream, grad, P.n_params, P.theta, P.m, P.v, P.beta_pow, make_hyper(c, 1));
+  launch_apply_adam(c->stream, grad, P.n_params, P.theta, P.m, P.v, P.beta_pow, make_hyper(c, 1), 1.f, pid);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -751,11 +759,11 @@ int ddrl_ppo_update_ddp(ddrl_ctx* c, int pid, const int32_t* shuffle, const int3
   for (int s = 0; s < steps; ++s) {
     if (ffn)
       launch_update_ffn(c->stream, c->d_ddp + s, h, m, inv_n, c->cfg.act_dim, P.d, P.lay.stride, c->cfg.leg_coupling,
-                        c->xchg, c->gx, 1, c->err);
+                        c->xchg, c->gx, grad_split(c, m), c->err, &c->upd_epoch);
     else
       launch_step_gnn(c->stream, ua[s], h, 0, m, inv_n, c->gnn);
     NCCLCHK(ncclAllReduce(P.grad, P.grad, (size_t)P.n_params, ncclFloat32, ncclSum, c->comm, c->stream));
-    launch_apply_adam(c->stream, P.grad, P.n_params, P.theta, P.m, P.v, P.beta_pow, h, gscale);
+    launch_apply_adam(c->stream, P.grad, P.n_params, P.theta, P.m, P.v, P.beta_pow, h, gscale, pid);
   }
   HIPCHK(hipGetLastError());
   // the pageable argument copy must not outlive ua (hipMemcpyAsync from pageable memory is

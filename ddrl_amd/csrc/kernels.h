@@ -130,12 +130,13 @@ struct UpdateHyper {
 // ksp: 1 = one workgroup per branch, 2 = row split over two (gx: gx_bytes(P) of exchange granules)
 // d / stride: the widest obs width / record stride of the launched policies
 void launch_update_ffn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHyper& h, int nrows, float inv_n, int A, int d,
-                       int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp, int* err);
+                       int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp, int* err,
+                       unsigned* epoch_ctr);   // per-context launch counter (granule tags)
 size_t gx_bytes(int P);
 // clip_by_global_norm + tf1 Adam on a flat (all-reduced) gradient vector
 // gscale multiplies the gradient before the clip (1 / ranks in the "local" data-parallel mode)
 void launch_apply_adam(hipStream_t s, const float* grad, int n, float* theta, float* m, float* v,
-                       float* beta_pow, const UpdateHyper& h, float gscale = 1.f);
+                       float* beta_pow, const UpdateHyper& h, float gscale = 1.f, int xcd = 0);
 
 // ---- ModelV2.forward / value_function on arbitrary rows ----
 struct ForwardArgs {

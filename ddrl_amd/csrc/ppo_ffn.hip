@@ -375,7 +375,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int f = 16 * tfa[i] + 4 * q + r, o = 16 * tfo[i] + c;
-      const bool ok = tv[i] && (i < NS1 || f < d);
+      const bool ok = tv[i] && (i < NS1 || f < d) && !U.grad_out;   // gradient-only launches: no Adam
       const int pidx = (i < NS1 ? bo.w2 : bo.w1) + f * 64 + o;
       mt[i][r] = ok ? U.m[pidx] : 0.f;
       vt4[i][r] = ok ? U.v[pidx] : 0.f;
@@ -387,7 +387,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   for (int k = 0; k < NSLOT; ++k) {
     const int e = tid + NT * k;
     ms[k] = vs[k] = 0.f;
-    if (e < nsb) {
+    if (e < nsb && !U.grad_out) {
       int pidx; float* lp;
       small_param<OB>(e, bo, W, pidx, lp);
       ms[k] = U.m[pidx];
@@ -865,7 +865,7 @@ static void launch_update_t(hipStream_t s, const UpdateBatch& ub, int P, int str
 
 void launch_update_ffn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHyper& h, int nrows, float inv_n,
                        int A, int d, int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp,
-                       int* err) {
+                       int* err, unsigned* epoch_ctr) {
   UpdateBatch ub;
   ub.a = ua_dev;
   ub.h = h;
@@ -874,11 +874,15 @@ void launch_update_ffn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHype
   ub.xchg = xchg;
   ub.gx = gx;
   ub.err = err;
-  static std::atomic<unsigned> launches{0};
-  ub.epoch = launches.fetch_add(1, std::memory_order_relaxed) % 4095u + 1u;
-  // clear the previous launch's granules (the epoch in every tag keeps them apart anyway)
-  (void)hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * 4 * ksp * h.P, s);
-  if (ksp == 2) (void)hipMemsetAsync(gx, 0, gx_bytes(h.P), s);
+  // Every granule tag carries the launch epoch (12 bits, per context). Granules are cleared
+  // only when the epoch wraps: between two clears every launch's epoch is larger than that
+  // of any granule left in the buffers, so a stale granule can never match.  (A memset per
+  // launch costs a fill kernel and a boundary, ~5 us, per data-parallel step.)
+  ub.epoch = (*epoch_ctr)++ % 4095u + 1u;
+  if (ub.epoch == 1) {
+    (void)hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * 8 * DDRL_MAXP, s);
+    (void)hipMemsetAsync(gx, 0, gx_bytes(DDRL_MAXP), s);
+  }
   if (cup)   // "cup": one shared leg policy, A = 2, d <= 20 (capi validate)
     launch_update_t<2, 5, true>(s, ub, h.P, stride, ksp);
   else
@@ -889,17 +893,53 @@ size_t gx_bytes(int P) { return sizeof(unsigned long long) * (size_t)P * 2 * 2 *
 
 // ------------------------------------------------------------------------------------
 // DDP apply: tf.clip_by_global_norm + tf1 Adam on an all-reduced flat gradient.
-// One workgroup; fixed-order reduction of the squared norm.
+// K = ceil(n / 1024) workgroups of 1024 threads.  Every workgroup computes the global norm
+// itself, in one fixed order (thread t sums elements t + 1024 k in k order, DPP within the
+// wave, the 16 wave sums in order), so all of them hold the same clip scale; workgroup b
+// then updates elements [1024 b, 1024 b + 1024).  The gradient is read K times, from L2.
+// beta_pow[2] counts the workgroups that have read beta1^t / beta2^t; the last to arrive
+// advances them and resets the count (the next launch on the stream starts after this one).
+// The grid is 8 K blocks of which only those on XCD `xcd` (block mod 8, the dispatcher's
+// round robin) work: the update kernel of the same policy runs on that XCD, so the gradient
+// it wrote and the weights it reads next stay in that XCD's L2 (spreading the slices over
+// all XCDs cost the next gradient launch 3 us of weight misses).
+// K = 0: one workgroup with a strided loop (vectors beyond 32 K elements).
 // ------------------------------------------------------------------------------------
+template <int K>
 __global__ void __launch_bounds__(1024) k_apply_adam(const float* __restrict__ grad, int n,
                                                      float* theta, float* m, float* v,
-                                                     float* beta_pow, UpdateHyper h, float gscale) {
+                                                     float* beta_pow, UpdateHyper h, float gscale, int xcd) {
   __shared__ float red[16];
+  if (K > 0 && (int)(blockIdx.x & 7) != xcd) return;   // not on the policy's XCD
   const int tid = threadIdx.x;
+  const float b1p = beta_pow[0], b2p = beta_pow[1];
+  const int i0 = K > 0 ? (int)(blockIdx.x >> 3) * 1024 + tid : tid;
+  const bool own = i0 < n;
+  float mm = 0.f, vv = 0.f, th = 0.f, go = 0.f;
+  if (K > 0 && own) {   // this workgroup's slice, issued with the norm loads
+    mm = m[i0];
+    vv = v[i0];
+    th = theta[i0];
+    go = grad[i0];
+  }
   float ss = 0.f;
-  for (int i = tid; i < n; i += 1024) {
-    const float gi = grad[i] * gscale;   // gscale: 1 / ranks of the "local" data-parallel mode
-    ss += gi * gi;
+  if constexpr (K > 0) {
+    float g[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int i = tid + 1024 * k;
+      g[k] = i < n ? grad[i] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const float gi = g[k] * gscale;   // gscale: 1 / ranks of the "local" data-parallel mode
+      ss += gi * gi;
+    }
+  } else {
+    for (int i = tid; i < n; i += 1024) {
+      const float gi = grad[i] * gscale;
+      ss += gi * gi;
+    }
   }
   ss = wave_sum(ss);
   if ((tid & 63) == 0) red[tid >> 6] = ss;
@@ -912,26 +952,55 @@ __global__ void __launch_bounds__(1024) k_apply_adam(const float* __restrict__ g
   }
   __syncthreads();
   const float scale = red[0];
-  const float b1p = beta_pow[0], b2p = beta_pow[1];
   const float alpha = h.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   const float c1 = 1.f - h.b1, c2 = 1.f - h.b2;
-  for (int i = tid; i < n; i += 1024) {
-    const float g = (grad[i] * gscale) * scale;
-    float mi = m[i], vi = v[i];
-    mi = mi + (g - mi) * c1;
-    vi = vi + (g * g - vi) * c2;
-    m[i] = mi;
-    v[i] = vi;
-    theta[i] = theta[i] - (mi * alpha) / (sqrtf(vi) + h.eps);
-  }
-  __syncthreads();
-  if (tid == 0) {
-    beta_pow[0] = b1p * h.b1;
-    beta_pow[1] = b2p * h.b2;
+  auto adam = [&](float gr, float& a, float& b, float& t) {
+    const float gg = (gr * gscale) * scale;
+    a = a + (gg - a) * c1;
+    b = b + (gg * gg - b) * c2;
+    t = t - (a * alpha) / (sqrtf(b) + h.eps);
+  };
+  if constexpr (K > 0) {
+    if (own) {
+      adam(go, mm, vv, th);
+      m[i0] = mm;
+      v[i0] = vv;
+      theta[i0] = th;
+    }
+    if (tid == 0) {   // every thread of this workgroup has read beta_pow (barriers above)
+      unsigned* cnt = reinterpret_cast<unsigned*>(beta_pow + 2);
+      if (atomicAdd(cnt, 1u) == (unsigned)(gridDim.x >> 3) - 1) {
+        beta_pow[0] = b1p * h.b1;
+        beta_pow[1] = b2p * h.b2;
+        *cnt = 0u;
+      }
+    }
+  } else {
+    for (int i = tid; i < n; i += 1024) {
+      float a = m[i], b = v[i], t = theta[i];
+      adam(grad[i], a, b, t);
+      m[i] = a;
+      v[i] = b;
+      theta[i] = t;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      beta_pow[0] = b1p * h.b1;
+      beta_pow[1] = b2p * h.b2;
+    }
   }
 }
 
 void launch_apply_adam(hipStream_t s, const float* grad, int n, float* theta, float* m, float* v,
-                       float* beta_pow, const UpdateHyper& h, float gscale) {
-  hipLaunchKernelGGL(k_apply_adam, dim3(1), dim3(1024), 0, s, grad, n, theta, m, v, beta_pow, h, gscale);
+                       float* beta_pow, const UpdateHyper& h, float gscale, int xcd) {
+  const int k = (n + 1023) / 1024;
+  xcd &= 7;
+  if (k <= 16)        // fcnet policies: 11,205 .. 15,057 parameters
+    hipLaunchKernelGGL(k_apply_adam<16>, dim3(8 * k), dim3(1024), 0, s, grad, n, theta, m, v, beta_pow, h, gscale,
+                       xcd);
+  else if (k <= 32)   // GraphNet: 28,869 parameters
+    hipLaunchKernelGGL(k_apply_adam<32>, dim3(8 * k), dim3(1024), 0, s, grad, n, theta, m, v, beta_pow, h, gscale,
+                       xcd);
+  else
+    hipLaunchKernelGGL(k_apply_adam<0>, dim3(1), dim3(1024), 0, s, grad, n, theta, m, v, beta_pow, h, gscale, 0);
 }
