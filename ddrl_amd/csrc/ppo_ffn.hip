@@ -90,6 +90,55 @@ __device__ void stage_branch(const float* __restrict__ th, int d, const BranchOf
   for (int i = threadIdx.x; i < 64 * OB; i += blockDim.x) W.wo[i] = th[bo.wo + i];
   for (int i = threadIdx.x; i < OB; i += blockDim.x) W.bo[i] = th[bo.bo + i];
 }
+// The same image with every weight load of a thread issued before the first LDS store (one
+// memory round trip instead of one per loop trip; NT = threads per workgroup, 256 or 512).
+template <int OB, int NT>
+__device__ __forceinline__ void stage_branch_batched(const float* __restrict__ th, int d, const BranchOff& bo,
+                                                     float* lds, NetLds& W, int ncup) {
+  static_assert((48 * 64) % NT == 0 && (64 * 64) % NT == 0, "staging split");
+  constexpr int N1 = 48 * 64 / NT, N2 = 64 * 64 / NT, NS = (64 * OB + OB + 128 + NT - 1) / NT;
+  W.w1 = lds; W.w2 = W.w1 + 48 * 64; W.b1 = W.w2 + 64 * 64; W.b2 = W.b1 + 64;
+  W.wo = W.b2 + 64; W.bo = W.wo + 64 * OB; W.cup = W.bo + OB;
+  const int t = threadIdx.x;
+  float a1[N1], a2[N2], as[NS];
+#pragma unroll
+  for (int k = 0; k < N1; ++k) {
+    const int i = t + NT * k;
+    a1[k] = (i >> 6) < d ? th[bo.w1 + i] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < N2; ++k) a2[k] = th[bo.w2 + t + NT * k];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {   // [wo 64 OB][bo OB][b1 64][b2 64]
+    int e = t + NT * k;
+    float x = 0.f;
+    if (e < 64 * OB) x = th[bo.wo + e];
+    else if ((e -= 64 * OB) < OB) x = th[bo.bo + e];
+    else if ((e -= OB) < 64) x = th[bo.b1 + e];
+    else if ((e -= 64) < 64) x = th[bo.b2 + e];
+    as[k] = x;
+  }
+  float ac = t < ncup ? th[bo.cup + t] : 0.f;   // ncup <= 8 < NT
+#pragma unroll
+  for (int k = 0; k < N1; ++k) {
+    const int i = t + NT * k;
+    W.w1[sidx(i >> 6, i & 63)] = a1[k];
+  }
+#pragma unroll
+  for (int k = 0; k < N2; ++k) {
+    const int i = t + NT * k;
+    W.w2[sidx(i >> 6, i & 63)] = a2[k];
+  }
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    int e = t + NT * k;
+    if (e < 64 * OB) W.wo[e] = as[k];
+    else if ((e -= 64 * OB) < OB) W.bo[e] = as[k];
+    else if ((e -= OB) < 64) W.b1[e] = as[k];
+    else if ((e -= 64) < 64) W.b2[e] = as[k];
+  }
+  if (t < ncup) W.cup[t] = ac;
+}
 #define BRANCH_LDS_FLOATS (48 * 64 + 64 * 64 + 128 + 64 * 16 + 16)   // multiple of 4 floats
 
 // "Small" parameters owned one per thread: [dWo 64*OB][dbo OB][db1 64][db2 64], then the
@@ -341,7 +390,6 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   static_assert(KSP == 1 || (NT == 256 && NP == gx_pairs(OB, NW) && NP <= GX_MAX_PAIRS), "exchange pairs");
 
   NetLds W;
-  stage_branch<OB>(U.theta, d, bo, lds, W, NCUP);
   constexpr int LD = ROWS + 8;              // feature-major image stride
   float* bufA = lds + BRANCH_LDS_FLOATS;    // feature-major [64][LD]: H1, then X
   float* bufB = bufA + 64 * LD;             // feature-major [64][LD]: dZ2, then dZ1
@@ -359,6 +407,17 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     row_l[t] = 16 * RT * w + 16 * t + c;               // row of this workgroup's share
     row_ok[t] = ROWS * kq + row_l[t] < ub.nrows;
   }
+
+  // ---- first step's records (LDS-DMA) in flight while the weights are staged ----
+  const int total_steps = U.n_epochs * U.nb;
+  const int last = U.max_steps >= 0 ? min(total_steps, U.step0 + U.max_steps) : total_steps;
+  // minibatch row of this lane's staging slot (tid < ROWS)
+  const int gr = ROWS * kq + tid;
+  const bool gok = tid < ROWS && gr < ub.nrows;
+  if (tid < ROWS) idxb[tid] = U.step0 < last && gok ? row_index(U, U.step0, gr, true) : 0;
+  __syncthreads();
+  if (U.step0 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, idxb, stg);
+  stage_branch_batched<OB, NT>(U.theta, d, bo, lds, W, NCUP);
 
   // ---- optimizer state of the parameters this lane owns ----
   // tile tt = 4 fa + fo; slots 0..NS1-1: dW2 tiles w + NW i;  then dW1 tiles w + NW i (if < 4 nf1).
@@ -403,16 +462,8 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   const float lo = 1.f - H.clip, hi = 1.f + H.clip;
   __syncthreads();
 
-  const int total_steps = U.n_epochs * U.nb;
-  const int last = U.max_steps >= 0 ? min(total_steps, U.step0 + U.max_steps) : total_steps;
   RowData<A, RT> cur;
-  // records of step0 -> stg, row indices of step0 + 1 -> idxb, of step0 + 2 -> nxt
-  // minibatch row of this lane's staging slot (tid < ROWS)
-  const int gr = ROWS * kq + tid;
-  const bool gok = tid < ROWS && gr < ub.nrows;
-  if (tid < ROWS) idxb[tid] = U.step0 < last && gok ? row_index(U, U.step0, gr, true) : 0;
-  __syncthreads();
-  if (U.step0 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, idxb, stg);
+  // records of step0 -> stg (issued above), row indices of step0 + 1 -> idxb, of step0 + 2 -> nxt
   wait_vmcnt0();
   __syncthreads();
   if (tid < ROWS) idxb[tid] = U.step0 + 1 < last && gok ? row_index(U, U.step0 + 1, gr, true) : 0;
