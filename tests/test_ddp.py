@@ -193,3 +193,42 @@ def test_merge_running_stats_order_and_identity():
     assert n == ref.n
     np.testing.assert_allclose(M, ref.M, rtol=1e-14)
     np.testing.assert_allclose(S, ref.S, rtol=1e-14)
+
+
+class _RecordingCtx:
+    """Stands in for native.Context: records the ddrl_ppo_update_ddp call and serves stats."""
+
+    def __init__(self, kl_rows):
+        self.calls, self.kl_rows = [], kl_rows
+
+    def ppo_update_ddp(self, pid, shuffle, perms, m, kl, gscale):
+        self.calls.append((pid, shuffle, perms, m, kl, gscale))
+
+    def ppo_stats(self, pid, n):
+        st = np.zeros((n, 8), np.float32)
+        st[:, 3] = self.kl_rows[:n]
+        return st
+
+
+@pytest.mark.parametrize("mode,m,gscale", [("split", 128, 1.0), ("local", 128, 1.0)])
+def test_native_learner_plumbing_world1(mode, m, gscale, monkeypatch):
+    """NativeDataParallelLearner hands the schedule to the library as the Python learner
+    would run it: int32 [epochs][nb] slots, rows per rank and gradient scale by mode, and the
+    KL of the last epoch's statistics (world 1: the all-reduce is the identity)."""
+    import torch.distributed as dist
+    from ddrl_amd.ddp import Comm, NativeDataParallelLearner
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        ctx = _RecordingCtx(np.array([0.01, 0.03, 0.02], np.float32))
+        lr = NativeDataParallelLearner(ctx, Comm("cpu"), 0, 128, mode)
+        sh, pe = lr.schedule(np.random.default_rng(0), 3 * 128, 2)
+        assert pe.shape == (2, 3) and pe.dtype == np.int32
+        kl = lr.learn(sh, pe.astype(np.int64), 0.2)
+        (pid, shuffle, perms, rows, klc, gs), = ctx.calls
+        assert pid == 0 and shuffle is sh and rows == m and klc == 0.2 and gs == gscale
+        assert perms.dtype == np.int32 and perms.flags.c_contiguous and np.array_equal(perms, pe)
+        np.testing.assert_allclose(kl, np.mean([0.01, 0.03, 0.02]), rtol=1e-6)
+    finally:
+        dist.destroy_process_group()
