@@ -117,3 +117,31 @@ def test_native_ddp_argument_errors(pg1):
     with pytest.raises(DdrlError, match="rows_per_rank"):
         ctx.ppo_update_ddp(0, sh, np.zeros((1, 1), np.int32), 200, 0.2, 1.0)
     ctx.close()
+
+
+def test_grad_launches_across_epoch_wrap():
+    """Exchange granules carry a 12-bit per-context launch epoch and are cleared only when it
+    wraps (every 4,095 update launches).  Alternate two minibatches over 4,100 gradient
+    launches (row split: the partial-gradient exchange is live) and check the launches
+    around the wrap against the first two: a stale granule taken for a fresh one would
+    mix the other minibatch's partial sums in."""
+    import torch
+    ctx, cfg, inst = make_ctx("QuantrupedMultiEnv_SharedDecentral", 32, 4)
+    rng = np.random.default_rng(3)
+    params = init_params(ctx, cfg, 5, head_scale=1.0)
+    run_rollout(ctx, cfg, inst, params, rng, _filt(cfg.obs_full_dim, rng), 4)
+    R = ctx.records_get(0).shape[0]
+    perm = torch.from_numpy(np.random.default_rng(9).permutation(R).astype(np.int32)).cuda()
+    rows = [perm[:128], perm[128:256]]
+    g = torch.zeros(ctx.n_params[0], device="cuda")
+    ref = []
+    for i in range(4100):
+        ctx.ppo_grad(0, rows[i & 1], 128, 0.2, g, -1)
+        if i < 2:
+            ctx.synchronize()
+            ref.append(g.clone())
+        elif 4093 <= i or i % 1024 == 0:
+            ctx.synchronize()
+            assert torch.equal(g, ref[i & 1]), f"gradient launch {i}"
+    assert not torch.equal(ref[0], ref[1])
+    ctx.close()
