@@ -187,7 +187,10 @@ int ddrl_ppo_grad(ddrl_ctx* ctx, int pid, const int32_t* rows_dev, int n_rows,
                   float kl_coeff, float* grad_dev, int stats_step);
 int ddrl_ppo_apply(ddrl_ctx* ctx, int pid, const float* grad_dev);
 
-/* RCCL communicator of a data-parallel learner (SURVEY 8(b) "ddrl_comm_init"): rank 0 makes
+/* RCCL communicator of a data-parallel learner (SURVEY 8(b) "ddrl_comm_init"; replaces the
+ * GPU-tower gradient averaging of RLlib's TrainTFMultiGPU, 3p execution/train_ops.py, which
+ * the reference sizes with ray.init(num_gpus=...) at train_experiment_1_architecture_on_flat.py:94
+ * and the commented config['num_gpus'] at :103-106).  Rank 0 makes
  * the unique id (DDRL_COMM_ID_BYTES bytes, handed to the other ranks by the caller, e.g. a
  * torch.distributed broadcast), every rank joins with its rank; one communicator per context,
  * on the context's device.  comm_allreduce sums n floats in place on the context's stream. */
