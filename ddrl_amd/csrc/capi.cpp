@@ -609,6 +609,12 @@ int ddrl_ppo_update(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const 
   for (int p = 0; p < c->cfg.n_policies; ++p) {
     if (!(mask & (1 << p))) continue;
     if (!shuffle[p] || !perm[p]) return fail("null shuffle/perm for a masked policy");
+    // every minibatch is a full slice of the shuffled batch (RLlib's multi-GPU loader refuses
+    // a batch smaller than one minibatch too); the kernels read shuffle[0 .. nb * 128)
+    if (c->pol[p].R < c->cfg.sgd_minibatch_size)
+      return fail("policy " + std::to_string(p) + ": the train batch holds " + std::to_string(c->pol[p].R) +
+                  " rows, fewer than one minibatch (sgd_minibatch_size " +
+                  std::to_string(c->cfg.sgd_minibatch_size) + ")");
     ua[n] = make_update(c, p, shuffle[p], perm[p], kl[p]);
     c->kl_last[p] = kl[p];
     ua[n].max_steps = max_steps;

@@ -45,6 +45,11 @@ ROLLOUT_ENVS = [
     ("QuantrupedMultiEnv_TwoSides", 20, 4),
     ("QuantrupedMultiEnv_SharedDecentralLegID", 24, 4),
     ("QuantrupedMultiEnv_SharedDecentralLegTransforms", 24, 4),
+    ("QuantrupedMultiEnv_TwoDiags", 21, 4),
+    ("QuantrupedMultiEnv_SingleNeighbor", 18, 4),
+    ("QuantrupedMultiEnv_SingleDiagonal", 18, 4),
+    ("QuantrupedMultiEnv_SingleToFront", 18, 4),
+    ("QuantrupedMultiEnv_FullyDecentralGlobalCost", 22, 4),
 ]
 
 
@@ -145,6 +150,8 @@ TVEL = {"env_config": {"target_velocity": [1.0]}}   # obs 44: body_target_x_vel 
     ("QuantrupedMultiEnv_Centralized", 48, 8, 2, None),
     ("QuantrupedMultiEnv_SharedDecentralLegID", 32, 4, 2, None),
     ("QuantrupedMultiEnv_TwoSides", 33, 4, 2, None),             # A = 4, d = 27; ragged envs
+    ("QuantrupedMultiEnv_TwoDiags", 35, 4, 2, None),             # A = 4, diagonal leg pairs
+    ("QuantrupedMultiEnv_SingleNeighbor", 34, 4, 2, None),       # d = 27, 4 policies; R = 136
     ("QuantrupedMultiEnv_FullyDecentral", 37, 5, 2, TVEL),        # d = 20 (TVel), 4 policies
     ("QuantrupedMultiEnv_Local", 40, 4, 2, TVEL),                 # d = 36 (TVel)
 ])
@@ -354,3 +361,17 @@ def test_rollout_fragment_matches_step_loop():
     assert fa[0] == fb[0] and np.array_equal(fa[1], fb[1]) and np.array_equal(fa[2], fb[2])
     ctx_a.close()
     ctx_b.close()
+
+
+def test_update_rejects_batch_smaller_than_a_minibatch():
+    """A policy whose train batch (frag_len x agents) holds fewer rows than
+    sgd_minibatch_size has no full minibatch: the update refuses it instead of reading past
+    the shuffle (30 envs x T 4 = 120 rows per leg policy)."""
+    import torch
+    from ddrl_amd.native import DdrlError
+    ctx, cfg, _ = make_ctx("QuantrupedMultiEnv_SingleNeighbor", 30, 4)
+    sh = [torch.zeros(120, dtype=torch.int32, device="cuda") for _ in range(4)]
+    pe = [torch.zeros((cfg.num_sgd_iter, 1), dtype=torch.int32, device="cuda") for _ in range(4)]
+    with pytest.raises(DdrlError, match="fewer than one minibatch"):
+        ctx.ppo_update(0xF, sh, pe, [0.2] * 4)
+    ctx.close()
