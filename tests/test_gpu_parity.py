@@ -50,6 +50,7 @@ ROLLOUT_ENVS = [
     ("QuantrupedMultiEnv_SingleDiagonal", 18, 4),
     ("QuantrupedMultiEnv_SingleToFront", 18, 4),
     ("QuantrupedMultiEnv_FullyDecentralGlobalCost", 22, 4),
+    ("QuantrupedMultiEnv_Centralized", 1, 200),   # C1: one env, a full 200-step fragment
 ]
 
 
@@ -152,6 +153,7 @@ TVEL = {"env_config": {"target_velocity": [1.0]}}   # obs 44: body_target_x_vel 
     ("QuantrupedMultiEnv_TwoSides", 33, 4, 2, None),             # A = 4, d = 27; ragged envs
     ("QuantrupedMultiEnv_TwoDiags", 35, 4, 2, None),             # A = 4, diagonal leg pairs
     ("QuantrupedMultiEnv_SingleNeighbor", 34, 4, 2, None),       # d = 27, 4 policies; R = 136
+    ("QuantrupedMultiEnv_Centralized", 1, 160, 2, None),         # C1 shape: one env, A = 8, d = 43
     ("QuantrupedMultiEnv_FullyDecentral", 37, 5, 2, TVEL),        # d = 20 (TVel), 4 policies
     ("QuantrupedMultiEnv_Local", 40, 4, 2, TVEL),                 # d = 36 (TVel)
 ])
