@@ -12,9 +12,13 @@ QuantrupedMultiEnv_Local configuration (4 independent per-leg fcnet 2x64 policie
   KL-coefficient update from the last epoch's mean KL (host).
 Multi-GPU: 4096 envs are sharded over the ranks (C3: independent policies, no collective);
 each rank is an independent learner on its shard ("replicas"), value = all ranks' env-steps
-divided by the slowest rank's time.
+divided by the slowest rank's time.  Shared-policy envs (--env QuantrupedMultiEnv_SharedDecentral,
+..._DecentralShared_Graph) train data-parallel over the ranks instead: the library's RCCL loop
+(ddrl_ppo_update_ddp) by default, DDRL_DDP_LOOP=python for the Python loop, --ddp-mode
+split | local (ddrl_amd/ddp.py).  DDRL_FORCE_DDP=1 runs that learner at one rank (under
+torchrun) and DDRL_DIST_BACKEND=gloo rehearses N ranks on one GPU.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 4096] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 4096] [--env NAME] [--no-cpu-baseline]
 """
 from __future__ import annotations
 
