@@ -365,7 +365,11 @@ def main():
     # (policy: obs, action, old logits, logp, adv; value: obs, vf, vt) + its shuffle index
     obs_len = 93 if gnn else d
     rec_bytes_launch = 4 * (2 * obs_len + 3 * A + 4 + 2) * rows_per_step * steps_per_policy * P
-    parallelism = (f"data-parallel over {world} ranks: RCCL all-reduce of the gradient every SGD step "
+    ddp_how = ("RCCL all-reduce of the gradient every SGD step, loop in the library (ddrl_ppo_update_ddp)"
+               if isinstance(learner, NativeDataParallelLearner) else
+               f"{'RCCL' if backend == 'nccl' else backend} all-reduce of the gradient every SGD step, Python loop") \
+        if ddp else ""
+    parallelism = (f"data-parallel over {world} ranks: {ddp_how} "
                    f"({args.ddp_mode} mode, {rows_per_step} rows per rank per step)" if ddp else
                    "replicas (no collective)")
     result = {
