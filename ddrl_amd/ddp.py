@@ -135,9 +135,15 @@ class DataParallelLearner:
         self.grad_scale = 1.0 if mode == "split" else 1.0 / comm.world
 
     def n_minibatches(self, rows_local):
-        """Steps per epoch: every rank must run the same number (the smallest shard wins)."""
-        nb = max(1, rows_local // self.rows_per_rank)
-        return int(self.comm.all_reduce_np(np.array([nb], np.int64), op="min")[0])
+        """Steps per epoch: every rank must run the same number (the smallest shard wins).
+        A shard without one full minibatch share is refused on every rank, as
+        ddrl_ppo_update refuses a batch smaller than one minibatch (a gradient launch reads
+        rows_per_rank rows of the shuffle)."""
+        nb = rows_local // self.rows_per_rank
+        nb = int(self.comm.all_reduce_np(np.array([nb], np.int64), op="min")[0])
+        if nb < 1:
+            raise ValueError(f"a rank holds fewer rows than one minibatch share of {self.rows_per_rank}")
+        return nb
 
     def schedule(self, rng, rows_local, epochs):
         nb = self.n_minibatches(rows_local)
