@@ -232,3 +232,39 @@ def test_native_learner_plumbing_world1(mode, m, gscale, monkeypatch):
         np.testing.assert_allclose(kl, np.mean([0.01, 0.03, 0.02]), rtol=1e-6)
     finally:
         dist.destroy_process_group()
+
+
+class _CommInitCtx:
+    def __init__(self):
+        self.args = None
+
+    def comm_init(self, uid, rank, world):
+        self.args = (bytes(uid), rank, world)
+
+
+def _comm_init_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    from ddrl_amd import ddp, native
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # rank 0's id: a recognizable pattern instead of ncclGetUniqueId (no GPU here)
+    native.comm_unique_id = lambda: bytes((7 * i + 3) % 256 for i in range(native.COMM_ID_BYTES))
+    ctx = _CommInitCtx()
+    ddp.native_comm_init(ctx, ddp.Comm("cpu"))
+    uid, r, w = ctx.args
+    np.savez(os.path.join(out_dir, f"c{rank}.npz"), uid=np.frombuffer(uid, np.uint8), rank=r, world=w)
+    dist.destroy_process_group()
+
+
+def test_native_comm_init_broadcasts_rank0_id_world2():
+    """native_comm_init at world 2 (gloo): every rank joins with rank 0's unique id, its own
+    rank and the world size (the RCCL join itself needs GPUs and runs on the GPU box)."""
+    import torch.multiprocessing as mp
+    out = tempfile.mkdtemp()
+    mp.spawn(_comm_init_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    want = np.array([(7 * i + 3) % 256 for i in range(128)], np.uint8)
+    for r in range(2):
+        got = np.load(os.path.join(out, f"c{r}.npz"))
+        np.testing.assert_array_equal(got["uid"], want)
+        assert int(got["rank"]) == r and int(got["world"]) == 2
