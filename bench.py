@@ -33,7 +33,9 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-METRIC = "env-steps/sec at 4096 envs × 4 leg agents; PPO update ms/minibatch"
+def metric_name(envs):
+    """BASELINE.json's metric, with the env count of this run (4096 = the metric's config)."""
+    return f"env-steps/sec at {envs} envs × 4 leg agents; PPO update ms/minibatch"
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense FP32 (MFMA f32 = vector rate), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01", "pmc_update.json")
@@ -143,8 +145,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) iteration")
     ap.add_argument("--cpu-envs", type=int, default=512)
-    ap.add_argument("--ddp-mode", default="local", choices=["split", "local"],
-                    help="shared-policy envs on N>1 GPUs: per-rank rows per SGD step (see ddrl_amd/ddp.py)")
+    ap.add_argument("--ddp-mode", default="split", choices=["split", "local"],
+                    help="shared-policy envs on N>1 GPUs: per-rank rows per SGD step (see ddrl_amd/ddp.py); "
+                         "split (default) = the reference's 128-row minibatch SGD, local = 128 rows per rank")
     args = ap.parse_args()
 
     import torch
@@ -203,7 +206,7 @@ def main():
     upd_ms = []
     if ddp:
         from ddrl_amd.ddp import (Comm, DataParallelLearner, HipBackend, NativeDataParallelLearner,
-                                  native_comm_init, sync_filters, sync_standardize)
+                                  native_comm_init, sync_standardize)
         comm = Comm(f"cuda:{local}" if backend == "nccl" else "cpu")
         if backend == "nccl" and os.environ.get("DDRL_DDP_LOOP", "native") == "native":
             # the minibatch loop inside the library on its own RCCL communicator
@@ -211,8 +214,6 @@ def main():
             learner = NativeDataParallelLearner(ctx, comm, 0, 128, args.ddp_mode)
         else:
             learner = DataParallelLearner(HipBackend(ctx), comm, 0, 128, args.ddp_mode)
-        filter_base = ctx.filter_get()
-        ctx.filter_delta_reset()
         grad = torch.zeros(ctx.n_params[0], dtype=torch.float32, device=f"cuda:{local}")
         sched_rng = np.random.default_rng(77 + rank)
 
@@ -251,10 +252,8 @@ def main():
             ctx.rollout_fragment(syn.obs, syn.eps, syn.fw, syn.cfrc, done, syn.actions)
         ctx.gae()
         if ddp:
-            nonlocal filter_base
-            filter_base = sync_filters(comm, filter_base, ctx.filter_delta_get())
-            ctx.filter_set(*filter_base)
-            ctx.filter_delta_reset()
+            # the env-side MeanStdFilter stays rank-local (a per-process singleton in the
+            # reference, simulation_envs/observation_filter.py:3-12: never synchronized)
             ctx.adv_norm_set(0, *sync_standardize(comm, ctx.adv_sums_get(0)))
             sh, pe = learner.schedule(sched_rng, R[0], E)
             sh_dev = torch.from_numpy(sh).to(stream.device)
@@ -373,7 +372,7 @@ def main():
                    f"({args.ddp_mode} mode, {rows_per_step} rows per rank per step)" if ddp else
                    "replicas (no collective)")
     result = {
-        "metric": METRIC,
+        "metric": metric_name(args.envs),
         "value": env_steps / t_max,
         "unit": "env-steps/s",
         "n_gpus": world,

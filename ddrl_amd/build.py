@@ -78,12 +78,25 @@ def _build(force, verbose, extra_flags):
     return LIB
 
 
+BOUNDS_LIB = os.path.join(HERE, "libddrl_hip_bounds.so")
+
+
+def build_bounds(force: bool = False, verbose: bool = False) -> str:
+    """The bounds-checked diagnostic library (-DDDRL_BOUNDS: run-time index checks in the
+    update kernel, counted instead of faulting; tools/bounds_check.py)."""
+    return build(force, verbose, extra_flags=["-DDDRL_BOUNDS"], lib=BOUNDS_LIB,
+                 build_dir=os.path.join(HERE, "_build_bounds"))
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--bounds", action="store_true", help="also build libddrl_hip_bounds.so")
     a = ap.parse_args(argv)
     print(build(a.force, a.verbose))
+    if a.bounds:
+        print(build_bounds(a.force, a.verbose))
 
 
 if __name__ == "__main__":

@@ -66,7 +66,6 @@ struct ddrl_ctx {
   uint8_t* done_tn = nullptr;
   float** stage_tab = nullptr;    // device array of per-policy stage pointers
   int32_t* zero_perm = nullptr;
-  UpdateArgs* d_uargs = nullptr;  // device copy of the per-workgroup update arguments
   unsigned long long* xchg = nullptr;  // norm^2 exchange granules of the update kernel
   unsigned long long* gx = nullptr;    // partial-gradient granules of the row-split update
   unsigned upd_epoch = 0;              // update launches so far (granule tag epochs)
@@ -77,8 +76,6 @@ struct ddrl_ctx {
   // host-variant staging
   float *h_obs = nullptr, *h_eps = nullptr, *h_act = nullptr;
   ncclComm_t comm = nullptr;           // data-parallel learner (ddrl_comm_init)
-  UpdateArgs* d_ddp = nullptr;         // per-step arguments of ddrl_ppo_update_ddp
-  size_t ddp_cap = 0;
   float *h_fw = nullptr, *h_cfrc = nullptr;
   uint8_t* h_done = nullptr;
   std::vector<void*> allocs;
@@ -221,7 +218,7 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
        dalloc(c, &c->f_dM, DDRL_MAXFULL) || dalloc(c, &c->f_dS, DDRL_MAXFULL) ||
        dalloc(c, &c->pf, (size_t)DDRL_MAXP * PF_STRIDE) || dalloc(c, &c->zs, 2 * DDRL_MAXFULL) || dalloc(c, &c->done_tn, (size_t)T * N) ||
        dalloc(c, &c->stage_tab, DDRL_MAXP) || dalloc(c, &c->zero_perm, 4) ||
-       dalloc(c, &c->d_uargs, DDRL_MAXP) || dalloc(c, &c->xchg, 8 * DDRL_MAXP) ||
+       dalloc(c, &c->xchg, 8 * DDRL_MAXP) ||
        dalloc(c, &c->gx, gx_bytes(DDRL_MAXP) / sizeof(unsigned long long)) || dalloc(c, &c->err, 1) ||
        dalloc(c, &c->h_obs, (size_t)N * g.obs_full_dim) ||
        dalloc(c, &c->h_eps, (size_t)N * g.n_agents * g.act_dim) || dalloc(c, &c->h_act, (size_t)N * 8) ||
@@ -256,7 +253,6 @@ int ddrl_ctx_destroy(ddrl_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
   if (c->comm) (void)ncclCommDestroy(c->comm);
-  if (c->d_ddp) (void)hipFree(c->d_ddp);
   for (void* p : c->allocs) (void)hipFree(p);
   delete c;
   return 0;
@@ -626,10 +622,9 @@ int ddrl_ppo_update(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const 
   int maxd = 0, maxs = 0;  // KS1 instance / staging rows must cover the widest policy
   for (int i = 0; i < n; ++i) maxd = std::max(maxd, ua[i].d), maxs = std::max(maxs, ua[i].lay.stride);
   UpdateHyper h = make_hyper(c, n);
-  // pageable source: the runtime stages (or blocks on) the copy before returning
-  HIPCHK(hipMemcpyAsync(c->d_uargs, ua, sizeof(UpdateArgs) * n, hipMemcpyHostToDevice, c->stream));
+  // the arguments travel by value in the kernel's argument block (no copy from this stack frame)
   if (c->cfg.model_kind == DDRL_MODEL_FFN)
-    launch_update_ffn(c->stream, c->d_uargs, h, 128, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim, maxd, maxs,
+    launch_update_ffn(c->stream, ua, h, 128, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim, maxd, maxs,
                       c->cfg.leg_coupling, c->xchg, c->gx, c->update_split, c->err, &c->upd_epoch);
   else if (c->pol[0].last_steps > 0) {   // one shared policy
     const int last = c->pol[0].last_steps;
@@ -678,9 +673,8 @@ int ddrl_ppo_grad(ddrl_ctx* c, int pid, const int32_t* rows, int n_rows, float k
   u.stats = stats_step >= 0 ? c->pol[pid].stats + (size_t)stats_step * 8 : nullptr;
   c->kl_last[pid] = kl;
   UpdateHyper h = make_hyper(c, 1);
-  HIPCHK(hipMemcpyAsync(c->d_uargs, &u, sizeof(UpdateArgs), hipMemcpyHostToDevice, c->stream));
   if (c->cfg.model_kind == DDRL_MODEL_FFN)
-    launch_update_ffn(c->stream, c->d_uargs, h, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim,
+    launch_update_ffn(c->stream, &u, h, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim,
                       c->pol[pid].d, c->pol[pid].lay.stride, c->cfg.leg_coupling, c->xchg, c->gx,
                       grad_split(c, n_rows), c->err, &c->upd_epoch);
   else
@@ -751,30 +745,22 @@ int ddrl_ppo_update_ddp(ddrl_ctx* c, int pid, const int32_t* shuffle, const int3
       ua[(size_t)e * nb + b] = u;
     }
   const bool ffn = c->cfg.model_kind == DDRL_MODEL_FFN;
-  if (ffn) {   // the fused kernel reads its arguments from device memory: all steps at once
-    if (c->ddp_cap < (size_t)steps) {
-      if (c->d_ddp) HIPCHK(hipFree(c->d_ddp));
-      c->d_ddp = nullptr;
-      c->ddp_cap = 0;
-      HIPCHK(hipMalloc(&c->d_ddp, sizeof(UpdateArgs) * (size_t)steps));
-      c->ddp_cap = steps;
-    }
-    HIPCHK(hipMemcpyAsync(c->d_ddp, ua.data(), sizeof(UpdateArgs) * (size_t)steps, hipMemcpyHostToDevice, c->stream));
-  }
   c->kl_last[pid] = kl;
   for (int s = 0; s < steps; ++s) {
     if (ffn)
-      launch_update_ffn(c->stream, c->d_ddp + s, h, m, inv_n, c->cfg.act_dim, P.d, P.lay.stride, c->cfg.leg_coupling,
+      launch_update_ffn(c->stream, &ua[s], h, m, inv_n, c->cfg.act_dim, P.d, P.lay.stride, c->cfg.leg_coupling,
                         c->xchg, c->gx, grad_split(c, m), c->err, &c->upd_epoch);
     else
       launch_step_gnn(c->stream, ua[s], h, 0, m, inv_n, c->gnn);
     NCCLCHK(ncclAllReduce(P.grad, P.grad, (size_t)P.n_params, ncclFloat32, ncclSum, c->comm, c->stream));
     launch_apply_adam(c->stream, P.grad, P.n_params, P.theta, P.m, P.v, P.beta_pow, h, gscale, pid);
   }
+  // every rank fails together: a norm-exchange timeout on one rank (whose zeroed gradient has
+  // already been summed into every rank's weights) is all-reduced (max) into every rank's
+  // error word, so no rank goes on to its next collective while another one raises
+  NCCLCHK(ncclAllReduce(c->err, c->err, 1, ncclInt32, ncclMax, c->comm, c->stream));
   HIPCHK(hipGetLastError());
-  // the pageable argument copy must not outlive ua (hipMemcpyAsync from pageable memory is
-  // staged before it returns on ROCm, but synchronize to be independent of that)
-  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));   // the error word of every step
   return check_err(c);
 }
 

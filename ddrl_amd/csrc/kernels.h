@@ -126,10 +126,11 @@ struct UpdateHyper {
   int vf_mode;
   int P;
 };
-// ua_dev: device array of h.P UpdateArgs (one persistent workgroup per entry)
+// ua: host array of h.P UpdateArgs (one persistent workgroup pair per entry), passed to the
+//     kernel by value in its argument block (no device copy, nothing outlives the call)
 // ksp: 1 = one workgroup per branch, 2 = row split over two (gx: gx_bytes(P) of exchange granules)
 // d / stride: the widest obs width / record stride of the launched policies
-void launch_update_ffn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHyper& h, int nrows, float inv_n, int A, int d,
+void launch_update_ffn(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n, int A, int d,
                        int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp, int* err,
                        unsigned* epoch_ctr);   // per-context launch counter (granule tags)
 size_t gx_bytes(int P);
@@ -137,6 +138,9 @@ size_t gx_bytes(int P);
 // gscale multiplies the gradient before the clip (1 / ranks in the "local" data-parallel mode)
 void launch_apply_adam(hipStream_t s, const float* grad, int n, float* theta, float* m, float* v,
                        float* beta_pow, const UpdateHyper& h, float gscale = 1.f, int xcd = 0);
+// Bounds-checked diagnostic build (-DDDRL_BOUNDS): violation counters of the update kernel's
+// staging / record / schedule / LDS indices (see ppo_ffn.hip); ddrl_diag_bounds reads them.
+#define DDRL_NBOUNDS 6
 
 // ---- ModelV2.forward / value_function on arbitrary rows ----
 struct ForwardArgs {

@@ -49,7 +49,7 @@ __host__ __device__ constexpr int gx_pairs(int OB, int NW) {
 #define GX_MAX_PAIRS 20
 
 struct UpdateBatch {
-  const UpdateArgs* a;   // device array, one entry per policy
+  UpdateArgs a[DDRL_MAXP];   // one entry per policy, by value in the kernel argument block
   UpdateHyper h;
   int nrows;             // rows per minibatch handled here (<= 128)
   float inv_n;           // 1 / sgd_minibatch_size (global minibatch)
@@ -57,7 +57,33 @@ struct UpdateBatch {
   unsigned long long* gx;    // [P][2 branches][KSP][2 parities][GX_MAX_PAIRS][256 lanes][2] partial-gradient granules
   int* err;              // set to 1 if an exchange timed out
   unsigned epoch;        // launch counter (12 bits, never 0): high bits of every exchange tag
+  unsigned lds_bytes;    // dynamic LDS of the launch (bounds-checked build)
 };
+
+// Bounds-checked diagnostic build (-DDDRL_BOUNDS, tools/build_diag.py): every staging,
+// record, schedule and LDS index the update kernel derives at run time is checked against its
+// buffer before use; a violation counts into g_bounds[k] and the access is clamped into range
+// (never faults).  k: 0 staging row of a gathered chunk, 1 record row index >= R, 2 schedule
+// index (perm / shuffle) out of range, 3 LDS-DMA destination past the launch's LDS, 4 staged
+// record read past the staging rows, 5 parameter index past n_params.
+#ifdef DDRL_BOUNDS
+__device__ unsigned g_bounds[DDRL_NBOUNDS];
+__device__ __forceinline__ bool bchk(bool ok, int k) {
+  if (!ok) atomicAdd(&g_bounds[k], 1u);
+  return ok;
+}
+extern "C" int ddrl_diag_bounds(unsigned* host, int reset) {
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bounds), sizeof(g_bounds)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned z[DDRL_NBOUNDS] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_bounds), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#define BCHK(cond, k) bchk((cond), (k))
+#else
+#define BCHK(cond, k) true
+#endif
 // Exchange tag of a step: the launch epoch above the step count, so a granule line some
 // cache still holds from an earlier launch can never carry a tag of this one.
 __device__ __forceinline__ unsigned xchg_tag(unsigned epoch, int step) {
@@ -177,18 +203,25 @@ struct RowData {
 // norm exchange (an early partner poll would otherwise wait for the gathers too).
 template <int NW, int ROWS>
 __device__ __forceinline__ void issue_rows(const float* rec, int stride, int cpr, int cpr_l, const int* idxb,
-                                           float* stg) {
+                                           float* stg, int R, unsigned lds_bytes) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (w == NW - 1) return;
   const int nchunk = ROWS * cpr_l;
   const float inv = 1.f / (float)cpr_l;
   for (int base = 64 * w; base < nchunk; base += 64 * (NW - 1)) {   // wave-uniform
     const int g = base + lane;
-    const int row = (int)(((float)g + 0.5f) * inv);
+    int row = (int)(((float)g + 0.5f) * inv);
     const int k = min(g - row * cpr_l, cpr - 1);
     const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr(stg + 4 * base));
-    if (g < nchunk) glds16(rec + (size_t)idxb[row] * stride + 4 * k, dst);
+    if (g < nchunk) {
+      if (!BCHK(row >= 0 && row < ROWS && k >= 0, 0)) row = 0;
+      int idx = idxb[row];
+      if (!BCHK(idx >= 0 && idx < R, 1)) idx = 0;
+      if (BCHK(dst + 16u * (unsigned)lane + 16u <= lds_bytes, 3))
+        glds16(rec + (size_t)idx * stride + 4 * k, dst);
+    }
   }
+  (void)R; (void)lds_bytes;
 }
 
 // staging-row chunks for a record of `stride` floats (the A = 8 kernels keep the plain
@@ -204,6 +237,16 @@ template <int A, int KS1, bool POL, int RT>
 __device__ __forceinline__ void load_row(const float* stg, int stg_stride, const RecLayout& L, const int* row_l,
                                          int d, RowData<A, RT>& r) {
   const int q = (threadIdx.x & 63) >> 4;
+#ifdef DDRL_BOUNDS
+  {
+    // the widest column this lane group reads (the generic KS1 = 12 instance reads columns < d
+    // only): it must lie inside the record, i.e. inside this row's staging slot
+    int hi = KS1 < 12 ? L.obs + 4 * KS1 - 1 : L.obs + d - 1;
+    if (POL) hi = max(max(hi, L.act + A - 1), max(L.logit + 2 * A - 1, max(L.logp, max(L.adv, L.cid))));
+    else hi = max(hi, max(L.vf, L.vt));
+    for (int t = 0; t < RT; ++t) BCHK(row_l[t] >= 0 && row_l[t] < DDRL_MB && hi < L.stride, 4);
+  }
+#endif
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
     const float* rp = stg + row_l[t] * stg_stride;
@@ -257,7 +300,14 @@ __device__ __forceinline__ void write_stats(float* so, const float* red, float n
 __device__ __forceinline__ int row_index(const UpdateArgs& U, int step, int row_l, bool ok) {
   if (!ok) return 0;
   const int e = step / U.nb, b = step - e * U.nb;
+#ifdef DDRL_BOUNDS
+  if (!BCHK(e >= 0 && e < U.n_epochs, 2)) return 0;
+  const int slot = gld(U.perm + e * U.nb + b);
+  if (!BCHK(slot >= 0 && slot < U.nb && (slot + 1) * DDRL_MB <= max(U.R, DDRL_MB) && row_l < DDRL_MB, 2)) return 0;
+  return gld(U.shuffle + slot * DDRL_MB + row_l);
+#else
   return gld(U.shuffle + gld(U.perm + e * U.nb + b) * DDRL_MB + row_l);
+#endif
 }
 // minibatch slot of a step (wave-uniform: perm[e][b])
 __device__ __forceinline__ int perm_slot(const UpdateArgs& U, int step) {
@@ -416,7 +466,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   const bool gok = tid < ROWS && gr < ub.nrows;
   if (tid < ROWS) idxb[tid] = U.step0 < last && gok ? row_index(U, U.step0, gr, true) : 0;
   __syncthreads();
-  if (U.step0 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, idxb, stg);
+  if (U.step0 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, idxb, stg, U.R, ub.lds_bytes);
   stage_branch_batched<OB, NT>(U.theta, d, bo, lds, W, NCUP);
 
   // ---- optimizer state of the parameters this lane owns ----
@@ -436,6 +486,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       const int f = 16 * tfa[i] + 4 * q + r, o = 16 * tfo[i] + c;
       const bool ok = tv[i] && (i < NS1 || f < d) && !U.grad_out;   // gradient-only launches: no Adam
       const int pidx = (i < NS1 ? bo.w2 : bo.w1) + f * 64 + o;
+      BCHK(!ok || (pidx >= 0 && pidx < of.n), 5);
       mt[i][r] = ok ? U.m[pidx] : 0.f;
       vt4[i][r] = ok ? U.v[pidx] : 0.f;
 
@@ -449,6 +500,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     if (e < nsb && !U.grad_out) {
       int pidx; float* lp;
       small_param<OB>(e, bo, W, pidx, lp);
+      BCHK(pidx >= 0 && pidx < of.n + NCUP, 5);
       ms[k] = U.m[pidx];
       vs[k] = U.v[pidx];
     }
@@ -660,7 +712,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     //      The row split issues them after its partner exchange instead: vmcnt retires in
     //      order, so the exchange loads would otherwise wait for the gathers.
 #ifndef DDRL_ABL_NO_PREFETCH
-    if (KSP == 1 && step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, idxb, stg);
+    if (KSP == 1 && step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, idxb, stg, U.R, ub.lds_bytes);
 #endif
     // the exchange lane (wave NW-1, which issued no gathers) polls the partner's granule
     // early: when the other branch is ahead, its norm^2 is already there at the exchange
@@ -705,7 +757,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 #pragma unroll
         for (int r = 0; r < 4; ++r) gt[i][r] += o[2 * NP0 + 4 * i + r];
 #ifndef DDRL_ABL_NO_PREFETCH
-      if (step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, idxb, stg);
+      if (step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, idxb, stg, U.R, ub.lds_bytes);
 #endif
       STAMP(14);
     } else {
@@ -905,20 +957,19 @@ static size_t update_lds_bytes(int O, int stride, int ksp) {
 }
 
 template <int A, int KS1, bool CUP = false>
-static void launch_update_t(hipStream_t s, const UpdateBatch& ub, int P, int stride, int ksp) {
+static void launch_update_t(hipStream_t s, UpdateBatch& ub, int P, int stride, int ksp) {
+  ub.lds_bytes = (unsigned)update_lds_bytes(2 * A, stride, ksp);
   if (ksp == 2)
-    hipLaunchKernelGGL((k_update_ffn<A, KS1, 2, CUP>), dim3(24 + P), dim3(64 * waves_for(A, 2)),
-                       update_lds_bytes(2 * A, stride, 2), s, ub);
+    hipLaunchKernelGGL((k_update_ffn<A, KS1, 2, CUP>), dim3(24 + P), dim3(64 * waves_for(A, 2)), ub.lds_bytes, s, ub);
   else
-    hipLaunchKernelGGL((k_update_ffn<A, KS1, 1, CUP>), dim3(8 + P), dim3(64 * waves_for(A, 1)),
-                       update_lds_bytes(2 * A, stride, 1), s, ub);
+    hipLaunchKernelGGL((k_update_ffn<A, KS1, 1, CUP>), dim3(8 + P), dim3(64 * waves_for(A, 1)), ub.lds_bytes, s, ub);
 }
 
-void launch_update_ffn(hipStream_t s, const UpdateArgs* ua_dev, const UpdateHyper& h, int nrows, float inv_n,
+void launch_update_ffn(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n,
                        int A, int d, int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp,
                        int* err, unsigned* epoch_ctr) {
   UpdateBatch ub;
-  ub.a = ua_dev;
+  for (int p = 0; p < DDRL_MAXP; ++p) ub.a[p] = p < h.P ? ua[p] : UpdateArgs{};
   ub.h = h;
   ub.nrows = nrows;
   ub.inv_n = inv_n;

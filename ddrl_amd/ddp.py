@@ -169,9 +169,22 @@ class DataParallelLearner:
         return self._kl(nb)
 
     def _kl(self, nb):
-        st = self.backend.stats(self.pid, nb)
-        kl_local = float(np.mean(st[:, 3].astype(np.float64)))
-        return float(self.comm.all_reduce_np(np.array([kl_local]))[0]) / self.comm.world
+        """All-reduced mean KL of the last epoch.  The error state of every rank is exchanged
+        first (max of a flag): a rank whose update kernel reported an error (norm-exchange
+        timeout) makes every rank raise, instead of the others blocking in their next
+        collective while it unwinds."""
+        err = None
+        try:
+            st = self.backend.stats(self.pid, nb)
+            kl_local = float(np.mean(st[:, 3].astype(np.float64)))
+        except Exception as e:   # the backend's own error (DdrlError from the C-ABI)
+            err, kl_local = e, 0.0
+        red = self.comm.all_reduce_np(np.array([kl_local, 1.0 if err is not None else 0.0]))
+        if red[1] > 0:
+            if err is not None:
+                raise err
+            raise RuntimeError(f"data-parallel update failed on {int(red[1])} other rank(s)")
+        return float(red[0]) / self.comm.world
 
 
 class NativeDataParallelLearner(DataParallelLearner):

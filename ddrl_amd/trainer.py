@@ -41,6 +41,14 @@ def leg_coupling_init(A):
     return np.resize(np.array([[1, 1], [-1, -1], [-1, -1], [1, 1]], np.float32), (4, A)).reshape(-1)
 
 
+def rank_seeds(seed, rank):
+    """(env seed, exploration-noise seed) of one rank: every rank samples its own trajectories
+    (like RLlib's rollout workers, whose envs are seeded per worker index), while the weights
+    come from `seed` alone and are identical on every rank.  Rank 0 keeps the single-process
+    seeds."""
+    return seed + 1_000_003 * rank, seed + 1 + 1_000_003 * rank
+
+
 class PPOTrainer:
     """Multi-agent PPO on one device (one env shard).
 
@@ -73,6 +81,7 @@ class PPOTrainer:
         P = self.cfg.n_policies
         self.rng = np.random.default_rng(seed)              # weights: identical on every rank
         self.sched_rng = np.random.default_rng(seed + 7919 * (self.rank + 1))
+        env_seed, noise_seed = rank_seeds(seed, self.rank)  # trajectories: different on every rank
         for p in range(P):
             if self.cfg.model_kind == N.MODEL_FFN:
                 theta = glorot_ffn_flat(self.rng, self.cfg.obs_dim[p], self.cfg.act_dim)
@@ -85,11 +94,11 @@ class PPOTrainer:
         self.kl_coeff = [float(c["kl_coeff"])] * P
         if env_backend is None:
             from .envs import SyntheticVecEnv
-            env_backend = SyntheticVecEnv(self.n_envs, self.cfg.obs_full_dim, self.device, seed=seed)
+            env_backend = SyntheticVecEnv(self.n_envs, self.cfg.obs_full_dim, self.device, seed=env_seed)
         self.backend = env_backend
         self.actions = torch.zeros((self.n_envs, 8), dtype=torch.float32, device=self.device)
         self.noise_gen = torch.Generator(device=self.device)
-        self.noise_gen.manual_seed(seed + 1)
+        self.noise_gen.manual_seed(noise_seed)
         self.timesteps_total = 0
         self.iteration = 0
         self.parallel = c.get("parallel") or ("ddp" if self.world > 1 and P == 1 else "replicas")
@@ -126,10 +135,15 @@ class PPOTrainer:
         self.ctx.gae()
         if self.parallel == "ddp":
             from .ddp import sync_filters, sync_standardize
-            merged = sync_filters(self.comm, self.filter_base, self.ctx.filter_delta_get())
-            self.ctx.filter_set(*merged)
-            self.ctx.filter_delta_reset()
-            self.filter_base = merged
+            # The env-side MeanStdFilter is a per-process singleton in the reference
+            # (simulation_envs/observation_filter.py:3-12) that RLlib never synchronizes: it stays
+            # rank-local unless the config asks for a merged one ("sync_env_filter": True, an
+            # extension).  RLlib's per-policy filters are synchronized (synchronize_filters).
+            if self.config.get("sync_env_filter", False):
+                merged = sync_filters(self.comm, self.filter_base, self.ctx.filter_delta_get())
+                self.ctx.filter_set(*merged)
+                self.ctx.filter_delta_reset()
+                self.filter_base = merged
             if self.pfilter_base is not None:   # RLlib synchronize_filters for the policy filters
                 for p in range(self.cfg.n_policies):
                     self.pfilter_base[p] = sync_filters(self.comm, self.pfilter_base[p],

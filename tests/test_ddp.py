@@ -268,3 +268,59 @@ def test_native_comm_init_broadcasts_rank0_id_world2():
         got = np.load(os.path.join(out, f"c{r}.npz"))
         np.testing.assert_array_equal(got["uid"], want)
         assert int(got["rank"]) == r and int(got["world"]) == 2
+
+
+class _FailingBackend:
+    """Gradient / apply do nothing; stats raise on the failing rank, as ddrl_ppo_stats does
+    when the update kernel's error word is set (norm-exchange timeout)."""
+
+    def __init__(self, fail):
+        self.fail = fail
+
+    def grad(self, pid, rows, n_rows, kl, grad, stats_step):
+        pass
+
+    def apply(self, pid, grad):
+        pass
+
+    def stats(self, pid, n):
+        if self.fail:
+            from ddrl_amd.native import DdrlError
+            raise DdrlError("update kernel: norm exchange between the policy and value workgroups timed out")
+        return np.zeros((n, 8), np.float32)
+
+
+def _error_worker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+    from ddrl_amd.ddp import Comm, DataParallelLearner
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = Comm("cpu")
+    learner = DataParallelLearner(_FailingBackend(rank == 1), comm, 0, MB, "split")
+    grad = torch.zeros(4)
+    msg = "no error"
+    try:
+        learner.learn(np.arange(256, dtype=np.int32), np.array([[0, 1], [1, 0]], np.int32), 0.2, grad)
+    except Exception as e:   # every rank must get here, none may hang in a collective
+        msg = f"{type(e).__name__}: {e}"
+    # one more collective after the failure: both ranks are still in step
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    with open(os.path.join(out_dir, f"e{rank}.txt"), "w") as f:
+        f.write(f"{msg}\n{float(t[0])}")
+    dist.destroy_process_group()
+
+
+def test_learner_error_raises_on_every_rank_world2():
+    """an update error on one rank (here rank 1's stats raise) makes every rank
+    raise after the learn loop (the error flag is all-reduced with the KL), and the ranks stay
+    in step for the next collective instead of one blocking while the other unwinds."""
+    import torch.multiprocessing as mp
+    out = tempfile.mkdtemp()
+    mp.spawn(_error_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    msgs = [open(os.path.join(out, f"e{r}.txt")).read().splitlines() for r in range(2)]
+    assert msgs[1][0].startswith("DdrlError") and "timed out" in msgs[1][0]
+    assert msgs[0][0].startswith("RuntimeError") and "other rank" in msgs[0][0]
+    assert msgs[0][1] == msgs[1][1] == "2.0"

@@ -145,7 +145,7 @@ def _params_close(got, ref, lr, steps, msg):
 TVEL = {"env_config": {"target_velocity": [1.0]}}   # obs 44: body_target_x_vel appended
 
 
-@pytest.mark.parametrize("env,n,T,steps,config", [
+UPDATE_CASES = [
     ("QuantrupedMultiEnv_Local", 64, 6, 3, None),
     ("QuantrupedMultiEnv_SharedDecentral", 32, 4, 2, None),
     ("QuantrupedMultiEnv_Centralized", 48, 8, 2, None),
@@ -156,7 +156,11 @@ TVEL = {"env_config": {"target_velocity": [1.0]}}   # obs 44: body_target_x_vel 
     ("QuantrupedMultiEnv_Centralized", 1, 160, 2, None),         # C1 shape: one env, A = 8, d = 43
     ("QuantrupedMultiEnv_FullyDecentral", 37, 5, 2, TVEL),        # d = 20 (TVel), 4 policies
     ("QuantrupedMultiEnv_Local", 40, 4, 2, TVEL),                 # d = 36 (TVel)
-])
+    ("QuantrupedMultiEnv_Centralized", 1, 200, 2, TVEL),         # C1 TVel: d = 44, A = 8, stride 76
+]
+
+
+@pytest.mark.parametrize("env,n,T,steps,config", UPDATE_CASES)
 def test_ppo_update_parity(env, n, T, steps, config):
     import torch
     ctx, cfg, inst = make_ctx(env, n, T, config)

@@ -99,3 +99,54 @@ def test_cup_model_reads_leg_features_and_sets_coupling():
     assert ModelCatalog.get("cup").__name__ == "FullyConnectedNetwork_Coupling_GlorotUniformInitializer"
     with pytest.raises(ValueError):
         make_cfg("QuantrupedMultiEnv_SharedDecentral", 4, 2, {"model": {"custom_model": "cup"}})
+
+
+# a5: GlorotUniformScaled (models/glorot_uniform_scaled_initializer.py:3-19) -- the product's
+# host init against the oracle's ffn_init / gnn_init: same draws in the same variable order
+# (bit-identical for one seed), limits sqrt(6 s / (fan_in + fan_out)) with s = 1 for hidden
+# kernels and 0.01 for the output heads, zero biases.
+@pytest.mark.parametrize("d,A", [(19, 2), (27, 2), (35, 2), (43, 8), (36, 2), (28, 4)])
+def test_glorot_ffn_init_matches_oracle(d, A):
+    from oracle import ddrl_oracle as O
+    from ddrl_amd.trainer import glorot_ffn_flat
+    shapes = O.ffn_param_shapes(d, 2 * A)
+    ref = O.pack(O.ffn_init(np.random.default_rng(5), d, 2 * A), shapes)
+    got = glorot_ffn_flat(np.random.default_rng(5), d, A)
+    assert got.dtype == np.float32 and got.shape == ref.shape
+    np.testing.assert_array_equal(got, ref)
+    parts = O.unpack(got, shapes)
+    for name, shape in shapes:
+        w = parts[name]
+        if name.endswith("bias"):
+            assert not w.any(), name
+            continue
+        s = 0.01 if name.startswith(("fc_out", "value_out")) else 1.0
+        lim = np.sqrt(6.0 * s / (shape[0] + shape[1]))
+        assert np.abs(w).max() <= lim and np.abs(w).max() > 0.9 * lim, name
+
+
+@pytest.mark.parametrize("A", [2, 4])
+def test_glorot_gnn_init_matches_oracle(A):
+    from oracle import ddrl_oracle as O
+    from ddrl_amd.models import glorot_gnn_flat
+    shapes = O.gnn_param_shapes(2 * A)
+    ref = O.pack(O.gnn_init(np.random.default_rng(6), 2 * A), shapes)
+    got = glorot_gnn_flat(np.random.default_rng(6), A)
+    np.testing.assert_array_equal(got, ref)
+    parts = O.unpack(got, shapes)
+    for name, shape in shapes:
+        w = parts[name]
+        if name.endswith("bias"):
+            assert not w.any(), name
+            continue
+        s = 0.01 if "linear_out" in name else 1.0
+        lim = np.sqrt(6.0 * s / (shape[0] + shape[1]))
+        assert np.abs(w).max() <= lim and np.abs(w).max() > 0.9 * lim, name
+
+
+def test_rank_seeds_differ_per_rank_and_keep_rank0():
+    from ddrl_amd.trainer import rank_seeds
+    seeds = [rank_seeds(3, r) for r in range(8)]
+    assert seeds[0] == (3, 4)                     # single-process seeds unchanged
+    flat = [s for pair in seeds for s in pair]
+    assert len(set(flat)) == len(flat)            # no two ranks (or streams) share a seed
