@@ -270,6 +270,34 @@ class PPOTrainer:
         meta = json.loads(bytes(z["meta"]).decode())
         self.iteration, self.timesteps_total = meta["iteration"], meta["timesteps_total"]
 
+    def restore_rllib(self, path):
+        """Load a published RLlib checkpoint (Results/**/checkpoint-1250, the file
+        evaluation/evaluate_trained_policies_pd.py:93-96 restores): per policy the Keras-order
+        weights, Adam m / v and beta powers, the RLlib MeanStdFilter RunningStat (when this
+        trainer runs observation_filter = MeanStdFilter) and the KL coefficient.  Read with the
+        no-code reader (ddrl_amd.rllib_checkpoint: a pickletools opcode walk; nothing in the
+        file is executed).  Returns the policy ids loaded."""
+        from .rllib_checkpoint import policy_ids, policy_state, read_checkpoint
+        ck = read_checkpoint(path)
+        have = policy_ids(ck)
+        missing = [pid for pid in self.policy_ids if pid not in have]
+        if missing:
+            raise ValueError(f"checkpoint has policies {have}, this env needs {self.policy_ids}")
+        for p, pid in enumerate(self.policy_ids):
+            st = policy_state(ck, pid)
+            if st["weights"].size != self.ctx.n_params[p]:
+                raise ValueError(f"{pid}: checkpoint holds {st['weights'].size} parameters, the model "
+                                 f"{self.ctx.n_params[p]}")
+            self.ctx.params_set(p, st["weights"])
+            self.ctx.adam_set(p, st["adam_m"], st["adam_v"], *st["beta_powers"])
+            if self.cfg.policy_filter and st["filter"] is not None:
+                self.ctx.policy_filter_set(p, *st["filter"])
+            if st["kl_coeff"] is not None:
+                self.kl_coeff[p] = st["kl_coeff"]
+        if self.parallel == "ddp" and self.pfilter_base is not None:
+            self.pfilter_base = [self.ctx.policy_filter_get(p) for p in range(self.cfg.n_policies)]
+        return list(self.policy_ids)
+
     def stop(self):
         self.ctx.close()
 

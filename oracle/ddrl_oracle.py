@@ -459,7 +459,7 @@ def ppo_loss_rows(logits, value, actions, old_logits, old_logp, vf_preds, adv, v
     """Per-row loss terms and analytic dL/dlogits, dL/dvalue for L = mean over rows.
     The tie rules follow TF's gradient kernels: tf.minimum routes to x where x <= y,
     tf.maximum to x where x >= y, clip_by_value passes for lo <= t <= hi."""
-    f = np.float32
+    f = F32
     logits = np.asarray(logits, f)
     n, A2 = logits.shape
     A = A2 // 2
@@ -514,10 +514,8 @@ def explained_variance(y, pred):
 # a15 / a16  clip_by_global_norm and tf1 Adam (training_ops ApplyAdam)
 # --------------------------------------------------------------------------------------
 def clip_by_global_norm(grads, clip_norm=0.5):
-    gn = np.float32(np.sqrt(np.sum([np.sum(np.square(g, dtype=np.float32)) for g in grads],
-                                   dtype=np.float32)))
-    scale = np.float32(clip_norm) * min(np.float32(1.0) / gn if gn > 0 else np.float32(np.inf),
-                                        np.float32(1.0) / np.float32(clip_norm))
+    gn = F32(np.sqrt(np.sum([np.sum(np.square(g, dtype=F32)) for g in grads], dtype=F32)))
+    scale = F32(clip_norm) * min(F32(1.0) / gn if gn > 0 else F32(np.inf), F32(1.0) / F32(clip_norm))
     return [(g * scale).astype(F32) for g in grads], gn
 
 
@@ -590,7 +588,7 @@ def ppo_update(model, params, shapes, adam, batch, shuffle, perms, kl_coeff, cfg
             dlogits, dvalue, st = ppo_loss_rows(
                 logits, value, batch["actions"][rows], batch["logits"][rows],
                 batch["logp"][rows], batch["vf_preds"][rows], batch["adv"][rows],
-                batch["vt"][rows], np.float32(kl_coeff), cfg.get("clip_param", 0.2),
+                batch["vt"][rows], F32(kl_coeff), cfg.get("clip_param", 0.2),
                 cfg.get("vf_clip_param", 10.0), cfg.get("vf_loss_coeff", 0.5),
                 cfg.get("entropy_coeff", 0.0))
             g = {"ffn": ffn_backward, "cup": cup_backward, "gnn": gnn_backward}[model](p, cache, dlogits, dvalue)
@@ -602,3 +600,16 @@ def ppo_update(model, params, shapes, adam, batch, shuffle, perms, kl_coeff, cfg
             out_stats.append(st)
             k += 1
     return unpack(theta, shapes), out_stats
+
+
+def with_dtype(dtype):
+    """A private copy of this module whose network arithmetic (forward, loss, backward, clip,
+    Adam, the minibatch loop) runs in `dtype` -- np.float64 gives the fp64 trajectory the
+    long-horizon parity tests measure fp32 rounding drift against.  Data preprocessing (GAE,
+    standardization, the filter) keeps its own fixed precisions."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(f"{__name__}_{np.dtype(dtype).name}", __file__)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    mod.F32 = np.dtype(dtype).type
+    return mod

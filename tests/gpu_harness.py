@@ -166,12 +166,17 @@ def synthetic_inputs(rng, cfg, T):
     return obs, eps, fw, cfrc, done
 
 
-def run_rollout(ctx, cfg, inst, params, rng, filt, T, orc_cls=None):
-    """Run the HIP rollout and the oracle on the same inputs; returns (oracle, inputs)."""
+def run_rollout(ctx, cfg, inst, params, rng, filt, T, orc_cls=None, pfilt=None):
+    """Run the HIP rollout and the oracle on the same inputs; returns (oracle, inputs).
+    pfilt: optional per-policy RLlib filter states [(n, M, S)] (cfg.policy_filter)."""
     import torch
     obs, eps, fw, cfrc, done = synthetic_inputs(rng, cfg, T)
     ctx.filter_set(*filt)
     orc = (orc_cls or OracleRollout)(cfg, inst, params, filt)
+    if pfilt is not None:
+        for p, (n, M, S) in enumerate(pfilt):
+            ctx.policy_filter_set(p, n, M, S)
+            orc.pf[p].n, orc.pf[p].M[:], orc.pf[p].S[:] = n, M, S
     dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
     actions = torch.zeros((cfg.n_envs, 8), dtype=torch.float32, device="cuda")
     acts_gpu = []
@@ -287,3 +292,30 @@ class GnnOracleRollout(OracleRollout):
 
     def bootstrap(self):
         self.last_v = [self._forward_all()[3]]
+
+
+def drift_check(got, model, params, shapes, batch, sh, pe, kl, steps, factor=4.0, floor=2e-7):
+    """Long-horizon parameter parity against the fp64 trajectory of the same algorithm.
+
+    Runs the oracle's minibatch loop in fp32 (numpy) and in fp64 (oracle.with_dtype) over the
+    same schedule; e32 = max |theta_fp32 - theta_fp64| is what fp32 rounding alone costs over
+    `steps` dependent steps.  The HIP parameters `got` must satisfy
+    max |got - theta_fp64| <= factor * e32 + floor and stay within 1e-5 of the fp32 oracle.
+    Returns (e32, egpu, max |got - theta_fp32|, fp64 per-step stats, fp64 params)."""
+    O64 = O.with_dtype(np.float64)
+    n = sum(int(np.prod(s)) for _, s in shapes)
+    new32, _ = O.ppo_update(model, params, shapes, O.Adam(n), batch, sh, pe, np.float32(kl),
+                            {"entropy_coeff": 0.0}, steps=steps)
+    p64 = {k: np.asarray(v, np.float64) for k, v in params.items()}
+    new64, st64 = O64.ppo_update(model, p64, shapes, O64.Adam(n), batch, sh, pe, kl, {"entropy_coeff": 0.0},
+                                 steps=steps)
+    th32 = O.pack(new32, shapes).astype(np.float64)
+    th64 = O64.pack(new64, shapes)
+    got = np.asarray(got, np.float64)
+    e32, egpu, d32 = np.abs(th32 - th64).max(), np.abs(got - th64).max(), np.abs(got - th32).max()
+    moved = np.abs(th64 - O.pack(params, shapes)).max()
+    print(f"\n{model} {steps} steps: max |theta moved| {moved:.3g}; max dev from fp64: numpy fp32 {e32:.3g}, "
+          f"HIP {egpu:.3g}; max |HIP - numpy fp32| {d32:.3g}")
+    assert egpu <= factor * e32 + floor, (egpu, e32)
+    assert d32 <= 1e-5, d32
+    return e32, egpu, d32, st64, new64

@@ -161,3 +161,24 @@ def test_cup_model_forward():
     with pytest.raises(ValueError):
         m.forward({"obs": (leg + 4, x)}, [], None)
     ctx.close()
+
+
+def test_cup_update_long_horizon():
+    """"cup" model over its whole 10-epoch schedule of a 1,280-row batch (100 fused steps)
+    against the fp64 trajectory (tests/gpu_harness.drift_check), coupling table included."""
+    import torch
+    from tests.gpu_harness import drift_check
+    n, T = 32, 10
+    ctx, cfg, params, orc, norms, _, _ = _rollout(n, T, 43, head_scale=1.0)
+    lay = ctx.layout[0]
+    ref = orc.flat_records(0, lay)
+    ctx.records_set(0, ref)
+    ctx.adv_norm_set(0, *norms[0])
+    sh, pe = O.sgd_schedule(np.random.default_rng(9), T * lay["C"], 128, cfg.num_sgd_iter)
+    steps = cfg.num_sgd_iter * (T * lay["C"] // 128)
+    assert steps == 100
+    ctx.ppo_update(1, [torch.from_numpy(sh).cuda()], [torch.from_numpy(pe).cuda()], [0.25])
+    ctx.synchronize()
+    shapes = O.cup_param_shapes(19, 2)
+    drift_check(ctx.params_get(0), "cup", params[0], shapes, _batch(ref, lay, 19, 2, norms[0]), sh, pe, 0.25, steps)
+    ctx.close()

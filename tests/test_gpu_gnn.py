@@ -154,3 +154,29 @@ def test_gnn_update_parity():
                s["grad_gnorm"]]
         _close(st[k, :7], np.array(ref, np.float32), rtol=1e-4, atol=1e-5, msg=f"stats step {k}")
     ctx.close()
+
+
+def test_gnn_update_long_horizon():
+    """The whole 10-epoch schedule of a 1,280-row batch (100 sequential grad / reduce / Adam
+    steps) against the fp64 trajectory (tests/gpu_harness.drift_check: HIP deviation <= 4x
+    the numpy fp32 deviation + 2e-7, and within 1e-5 of the fp32 oracle); learner statistics
+    of every step within 1e-4 relative of the fp64 ones."""
+    import torch
+    from tests.gpu_harness import drift_check
+    ctx, cfg, orc, norms, params, _, _ = _rollout(32, 10, 61, head_scale=1.0)   # R = 1280, nb = 10
+    lay = ctx.layout[0]
+    rec = orc.flat_records(0, lay)
+    ctx.records_set(0, rec)
+    ctx.adv_norm_set(0, *norms[0])
+    sh, pe = O.sgd_schedule(np.random.default_rng(7), rec.shape[0], 128, cfg.num_sgd_iter)
+    steps = cfg.num_sgd_iter * (rec.shape[0] // 128)
+    assert steps == 100
+    ctx.ppo_update(1, [torch.from_numpy(sh).cuda()], [torch.from_numpy(pe).cuda()], [0.2])
+    ctx.synchronize()
+    _, _, _, st64, _ = drift_check(ctx.params_get(0), "gnn", params, SHAPES, _batch(rec, lay, norms[0]), sh, pe,
+                                   0.2, steps)
+    st = ctx.ppo_stats(0, steps).astype(np.float64)
+    for col, k in [(1, "policy_loss"), (2, "vf_loss"), (3, "kl"), (4, "entropy"), (6, "grad_gnorm")]:
+        ref = np.array([s[k] for s in st64])
+        assert np.all(np.abs(st[:, col] - ref) <= 1e-4 * np.abs(ref) + 1e-6), k
+    ctx.close()

@@ -13,6 +13,7 @@ Tolerances (fp32 path, float64 filter/GAE as in the reference):
 import numpy as np
 import pytest
 
+from ddrl_amd import native as N
 from oracle import ddrl_oracle as O
 from tests.gpu_harness import init_params, make_ctx, run_rollout
 
@@ -68,8 +69,18 @@ def test_rollout_gae_parity_target_velocity(env, n, T):
     _rollout_gae_parity(env, n, T, {"env_config": {"target_velocity": [1.0]}})
 
 
+@pytest.mark.parametrize("env,n,T", [("QuantrupedMultiEnv_FullyDecentral", 24, 5),
+                                     ("QuantrupedMultiEnv_Local", 19, 4)])
+def test_rollout_gae_parity_norm_reward(env, n, T):
+    """norm_reward (quantruped_adaptor_multi_environment.py:173-186, DDRL_REWARD_NORM): every
+    leg gets the whole forward reward minus n_agents x its own control + contact cost."""
+    _rollout_gae_parity(env, n, T, {"env_config": {"norm_reward": True}})
+
+
 def _rollout_gae_parity(env, n, T, config):
     ctx, cfg, inst = make_ctx(env, n, T, config)
+    if config and config.get("env_config", {}).get("norm_reward"):
+        assert cfg.reward_mode == N.REWARD_NORM and inst.reward_mode == "norm"
     rng = np.random.default_rng(11)
     params = init_params(ctx, cfg, 3)
     orc, norms, a_gpu, a_orc = run_rollout(ctx, cfg, inst, params, rng, _filt(cfg.obs_full_dim, rng), T)
