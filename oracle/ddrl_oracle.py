@@ -564,10 +564,11 @@ def update_kl(kl_coeff, sampled_kl, kl_target=0.01):
     return kl_coeff
 
 
-def ppo_update(model, params, shapes, adam, batch, shuffle, perms, kl_coeff, cfg, steps=None):
+def ppo_update(model, params, shapes, adam, batch, shuffle, perms, kl_coeff, cfg, steps=None, snapshots=None):
     """Runs the minibatch loop for one policy.  `model` is "ffn", "cup" or "gnn".  `batch` is
     a dict of row arrays: obs (+ leg for "cup"; X/node_idx for "gnn"), actions, logits, logp, vf_preds, adv
-    (already standardized) and vt.  Returns (params, per-step stats list)."""
+    (already standardized) and vt.  Returns (params, per-step stats list).  `snapshots`: an
+    optional dict {step count: None} filled with the flat parameters after that many steps."""
     mb = cfg.get("sgd_minibatch_size", 128)
     epochs, nb = perms.shape
     theta = pack(params, shapes)
@@ -599,6 +600,8 @@ def ppo_update(model, params, shapes, adam, batch, shuffle, perms, kl_coeff, cfg
             st["grad_gnorm"] = float(gn)
             out_stats.append(st)
             k += 1
+            if snapshots is not None and k in snapshots:
+                snapshots[k] = theta.copy()
     return unpack(theta, shapes), out_stats
 
 

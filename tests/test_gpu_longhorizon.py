@@ -3,27 +3,28 @@
 BASELINE C2/C3 workload: QuantrupedMultiEnv_Local, 4096 envs x T = 200 -> R = 819,200 rows per
 policy, nb = 6,400 minibatches per epoch.  The fused update launch runs all four policies as
 the bench does (mask 0xF) and policy 0 is compared with the oracle over the same shuffle /
-permutation (train_experiment_1_architecture_on_flat.py:116,133-134) at the
-horizons H = 10, 100, 400, 1600, 3200 and 6400 sequential SGD steps (6400 = one full epoch).
+permutation (train_experiment_1_architecture_on_flat.py:116,133-134) after
+H = 10, 100, 400, 1600, 3200 and 6400 sequential SGD steps (6400 = one full epoch).
 
-Drift bound (a function of H, derived from measured fp32 rounding).  Two fp32 implementations
-of the same H-step recursion do not agree to the last bit: every step's rounding feeds the
-next.  Each horizon is therefore measured against the fp64 trajectory of the same algorithm
-(oracle.with_dtype(np.float64)):
-    e32(H)  = max |theta_numpy_fp32 - theta_fp64|   (what fp32 rounding alone costs)
-    egpu(H) = max |theta_HIP - theta_fp64|
-and every horizon requires egpu(H) <= 4 e32(H) + 2e-7 (the kernel's hardware tanh / exp / rcp /
-sqrt approximations, |err| ~1.5e-7 each, are per-step noise of the order of numpy's correctly
-rounded functions).  Measured on MI355X (r02): e32 / egpu = 6.9e-8 / 1.6e-7 (H = 10),
-1.6e-7 / 1.8e-7 (100), 3.7e-6 / 4.1e-6 (400), 4.1e-6 / 4.5e-6 (1600); at 6400 the trajectory
-itself bifurcates (a minibatch row's PPO ratio or value clip switches branch: the fp32
-trajectories leave the fp64 one by ~2e-2 -- numpy 0.0205, HIP 0.015 -- and only 0.6 % of numpy's
-parameters stay within 1e-5), so no fp32 implementation meets an absolute bar there.
-Absolute bars where they are meaningful (H <= 1600, before the bifurcation): every parameter
-within 1e-5 of fp64 (north_star) and within 1e-6 of numpy fp32; per-step learner statistics
-within 1e-4 relative (+1e-6 absolute) of fp64.  At H = 6400 the trained policy's outputs on
-4,096 sampled rows and the epoch-mean statistics (what update_kl consumes) must be no farther
-from the fp64 trajectory than 4x numpy fp32's distance (+1e-6).
+Drift bound, a function of H derived from measured fp32 rounding.  Two fp32 implementations of
+one H-step recursion do not agree to the last bit: every step's rounding feeds the next.  Each
+horizon is measured against the fp64 trajectory of the same algorithm (oracle.with_dtype):
+  * deterministic regime, H <= 1600: e32(H) = max |theta_numpy_fp32 - theta_fp64| is what fp32
+    rounding alone costs; the HIP parameters must satisfy max |theta_HIP - theta_fp64| <=
+    4 e32(H) + 2e-7 (the hardware tanh / exp / rcp / sqrt approximations, |err| ~1.5e-7, are
+    per-step noise of the order of numpy's correctly rounded functions), every parameter
+    within 1e-5 of fp64 (north_star) and within 1e-6 of numpy fp32, and every per-step learner
+    statistic within 1e-4 relative (+1e-6 absolute) of fp64.  Measured (MI355X, r02): e32 / HIP
+    6.9e-8 / 1.6e-7 (H = 10), 1.6e-7 / 1.8e-7 (100), 3.7e-6 / 4.1e-6 (400), 4.1e-6 / 4.5e-6 (1600).
+  * after the bifurcation (between 1,600 and 3,200 steps a minibatch row's ratio / value clip
+    switches branch in fp32 but not in fp64: every fp32 trajectory leaves the fp64 one by
+    ~1e-2 and only ~1 % of parameters stay within 1e-5 -- numpy and HIP alike, and they stay
+    within 5.4e-7 of each other at 3200), no fp32 implementation meets an absolute bar.  The
+    bar is the spread of fp32 trajectories: three more numpy fp32 runs that sum each
+    minibatch's rows in a different (fixed, permuted) order -- the same mathematics, other
+    roundings -- give s(H) = max over the four numpy runs of the distance to fp64, for the
+    parameters, the trained policy's outputs on 4,096 sampled rows, and the epoch means of the
+    learner statistics (what update_kl consumes); HIP must be within 2 s(H) (+2e-7).
 """
 import numpy as np
 import pytest
@@ -53,6 +54,23 @@ def _batch(rec, lay, d, A, norm):
                 vt=rec[:, lay["vt"]])
 
 
+def _row_order_variant(shuffle, seed):
+    """The same minibatches with their 128 rows in another order (fp32 sums reassociated)."""
+    order = np.random.default_rng(seed).permutation(128)
+    nb = shuffle.size // 128
+    out = shuffle.copy()
+    out[:nb * 128] = shuffle[:nb * 128].reshape(nb, 128)[:, order].reshape(-1)
+    return out
+
+
+def _run(mod, params, shapes, batch, sh, pe, horizons):
+    n = sum(int(np.prod(s)) for _, s in shapes)
+    snaps = {h: None for h in horizons}
+    _, stats = mod.ppo_update("ffn", params, shapes, mod.Adam(n), batch, sh, pe, 0.2, {}, steps=max(horizons),
+                              snapshots=snaps)
+    return {h: np.asarray(v, np.float64) for h, v in snaps.items()}, stats
+
+
 def test_one_epoch_local_fullsize_against_fp64_trajectory():
     import torch
     from ddrl_amd.synthetic import SyntheticRollout
@@ -72,10 +90,12 @@ def test_one_epoch_local_fullsize_against_fp64_trajectory():
     lay = ctx.layout[p]
     batch = _batch(ctx.records_get(p), lay, d, A, ctx.adv_norm_get(p))
     shapes = O.ffn_param_shapes(d, 2 * A)
-    n = sum(int(np.prod(s)) for _, s in shapes)
     sh, pe = sched[p]
     O64 = O.with_dtype(np.float64)
-    p64 = {k: v.astype(np.float64) for k, v in params[p].items()}
+    th64, st64 = _run(O64, {k: v.astype(np.float64) for k, v in params[p].items()}, shapes, batch, sh, pe, HORIZONS)
+    late = [h for h in HORIZONS if h > ABS_BAR_UNTIL]
+    runs32 = [_run(O, params[p], shapes, batch, sh, pe, HORIZONS)]
+    runs32 += [_run(O, params[p], shapes, batch, _row_order_variant(sh, 90 + k), pe, late) for k in range(3)]
     theta0 = [ctx.params_get(q) for q in range(4)]
     for H in HORIZONS:
         for q in range(4):      # same start for every horizon (the schedule restarts at step 0)
@@ -84,41 +104,41 @@ def test_one_epoch_local_fullsize_against_fp64_trajectory():
         ctx.ppo_update(0xF, dsh, dpe, [0.2] * 4, max_steps=H)
         ctx.synchronize()
         got = ctx.params_get(p).astype(np.float64)
-        new32, st32 = O.ppo_update("ffn", params[p], shapes, O.Adam(n), batch, sh, pe, 0.2, {}, steps=H)
-        new64, st64 = O64.ppo_update("ffn", p64, shapes, O64.Adam(n), batch, sh, pe, 0.2, {}, steps=H)
-        th32 = O.pack(new32, shapes).astype(np.float64)
-        th64 = O64.pack(new64, shapes)
-        e32, egpu, d32 = np.abs(th32 - th64).max(), np.abs(got - th64).max(), np.abs(got - th32).max()
-        print(f"\nH={H}: max dev from fp64: numpy fp32 {e32:.3g} ({np.mean(np.abs(th32 - th64) <= 1e-5):.4f} "
-              f"within 1e-5), HIP {egpu:.3g} ({np.mean(np.abs(got - th64) <= 1e-5):.4f}); "
-              f"max |HIP - numpy fp32| {d32:.3g}", flush=True)
-        assert egpu <= 4 * e32 + 2e-7, (H, egpu, e32)
+        egpu = np.abs(got - th64[H]).max()
+        e32s = [np.abs(r[0][H] - th64[H]).max() for r in runs32 if H in r[0]]
+        d32 = np.abs(got - runs32[0][0][H]).max()
+        print(f"\nH={H}: max dev from fp64: numpy fp32 runs {[f'{e:.3g}' for e in e32s]}, HIP {egpu:.3g} "
+              f"({np.mean(np.abs(got - th64[H]) <= 1e-5):.4f} within 1e-5); max |HIP - numpy fp32| {d32:.3g}",
+              flush=True)
         st = ctx.ppo_stats(p, H).astype(np.float64)
         if H <= ABS_BAR_UNTIL:
+            assert egpu <= 4 * e32s[0] + 2e-7, (H, egpu, e32s)
             assert egpu <= 1e-5 and d32 <= 1e-6, (H, egpu, d32)
             for col, k in STAT_KEYS:
-                ref = np.array([s[k] for s in st64])
+                ref = np.array([s[k] for s in st64[:H]])
                 dev = np.abs(st[:, col] - ref)
-                print(f"  {k}: max |HIP - fp64| {dev.max():.3g} (|ref| median {np.median(np.abs(ref)):.3g})")
-                assert np.all(dev <= 1e-4 * np.abs(ref) + 1e-6), (H, k)
-    # H = 6400 (one epoch): outputs and epoch-mean statistics relative to numpy fp32's distance
-    assert np.abs(th64 - O.pack(params[p], shapes)).max() > 0.1       # the policy did train
+                assert np.all(dev <= 1e-4 * np.abs(ref) + 1e-6), (H, k, dev.max())
+        else:
+            assert egpu <= 2 * max(e32s) + 2e-7, (H, egpu, e32s)
+    # H = 6400: the trained policy's outputs and the epoch-mean statistics against the spread
+    assert np.abs(th64[6400] - O.pack(params[p], shapes)).max() > 0.1       # the policy did train
     rows = np.random.default_rng(1).choice(R, 4096, replace=False)
     x = torch.from_numpy(np.ascontiguousarray(batch["obs"][rows])).cuda()
     lg = torch.zeros((4096, 2 * A), device="cuda")
     vv = torch.zeros(4096, device="cuda")
     ctx.policy_forward(p, x, 4096, lg, vv)
     ctx.synchronize()
-    l64, v64, _ = O64.ffn_forward(new64, batch["obs"][rows])
-    l32, v32, _ = O.ffn_forward(new32, batch["obs"][rows])
-    for name, g, r64, r32 in (("logits", lg.cpu().numpy(), l64, l32), ("value", vv.cpu().numpy(), v64, v32)):
-        dg, dn = np.abs(g - r64).max(), np.abs(r32 - r64).max()
-        print(f"{name} vs fp64: HIP {dg:.3g}, numpy fp32 {dn:.3g}")
-        assert dg <= 4 * dn + 1e-6, name
+    out64 = O64.ffn_forward(O64.unpack(th64[6400], shapes), batch["obs"][rows])[:2]
+    outs32 = [O.ffn_forward(O.unpack(r[0][6400].astype(np.float32), shapes), batch["obs"][rows])[:2] for r in runs32]
+    for i, (name, g) in enumerate((("logits", lg.cpu().numpy()), ("value", vv.cpu().numpy()))):
+        dg = np.abs(g - out64[i]).max()
+        spread = max(np.abs(o[i] - out64[i]).max() for o in outs32)
+        print(f"{name} vs fp64: HIP {dg:.3g}, fp32 spread {spread:.3g}")
+        assert dg <= 2 * spread + 2e-7, name
     for col, k in STAT_KEYS:
         ref = np.mean([s[k] for s in st64])
         dg = abs(st[:, col].mean() - ref)
-        dn = abs(np.mean([s[k] for s in st32]) - ref)
-        print(f"epoch mean {k}: |HIP - fp64| {dg:.3g}, |numpy fp32 - fp64| {dn:.3g} (ref {ref:.4g})")
-        assert dg <= 4 * dn + 1e-6 * abs(ref) + 1e-9, k
+        spread = max(abs(np.mean([s[k] for s in r[1]]) - ref) for r in runs32)
+        print(f"epoch mean {k}: |HIP - fp64| {dg:.3g}, fp32 spread {spread:.3g} (ref {ref:.4g})")
+        assert dg <= 2 * spread + 2e-7 * abs(ref), k
     ctx.close()
