@@ -83,8 +83,9 @@ BOUNDS_LIB = os.path.join(HERE, "libddrl_hip_bounds.so")
 
 def build_bounds(force: bool = False, verbose: bool = False) -> str:
     """The bounds-checked diagnostic library (-DDDRL_BOUNDS: run-time index checks in the
-    update kernel, counted instead of faulting; tools/bounds_check.py)."""
-    return build(force, verbose, extra_flags=["-DDDRL_BOUNDS"], lib=BOUNDS_LIB,
+    update kernel, counted instead of faulting; tools/bounds_check.py), with the exchange
+    granules as relaxed agent-scope atomics (-DDDRL_XCHG_ATOMIC, the formally defined protocol)."""
+    return build(force, verbose, extra_flags=["-DDDRL_BOUNDS", "-DDDRL_XCHG_ATOMIC"], lib=BOUNDS_LIB,
                  build_dir=os.path.join(HERE, "_build_bounds"))
 
 

@@ -70,6 +70,7 @@ struct ddrl_ctx {
   unsigned long long* gx = nullptr;    // partial-gradient granules of the row-split update
   unsigned upd_epoch = 0;              // update launches so far (granule tag epochs)
   int update_split = 2;                // workgroups per branch of the fused update (1 or 2)
+  int xchg_coherent = 0;               // 1: device-coherent exchange stores (DDRL_XCHG_COHERENT=1)
   int* err = nullptr;                  // device error word (exchange timeout)
   float kl_last[DDRL_MAXP] = {0};
   GnnScratch gnn{};               // GraphNet step scratch (per-tile partial gradients, ...)
@@ -166,6 +167,9 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
   ddrl_ctx* c = new ddrl_ctx();
   // fused update geometry: DDRL_UPDATE_SPLIT=1 keeps one workgroup per branch (timing / A-B)
   if (const char* e = std::getenv("DDRL_UPDATE_SPLIT")) c->update_split = std::atoi(e) == 1 ? 1 : 2;
+  // exchange protocol of the fused update: the XCD-local L2 protocol by default (every
+  // workgroup checks its placement), device-coherent stores with DDRL_XCHG_COHERENT=1
+  if (const char* e = std::getenv("DDRL_XCHG_COHERENT")) c->xchg_coherent = std::atoi(e) == 1;
   c->cfg = *cfg;
   c->device = device;
   const ddrl_cfg& g = c->cfg;
@@ -269,6 +273,9 @@ static int check_err(ddrl_ctx* c) {
   HIPCHK(hipMemcpy(&e, c->err, sizeof(int), hipMemcpyDeviceToHost));
   if (e) {
     (void)hipMemset(c->err, 0, sizeof(int));
+    if (e == 2)
+      return fail("update kernel: a workgroup was not placed on its policy's XCD, so the XCD-local exchange "
+                  "protocol cannot run (rerun with DDRL_XCHG_COHERENT=1: device-coherent exchange stores)");
     return fail("update kernel: norm exchange between the policy and value workgroups timed out");
   }
   return 0;
@@ -625,7 +632,7 @@ int ddrl_ppo_update(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const 
   // the arguments travel by value in the kernel's argument block (no copy from this stack frame)
   if (c->cfg.model_kind == DDRL_MODEL_FFN)
     launch_update_ffn(c->stream, ua, h, 128, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim, maxd, maxs,
-                      c->cfg.leg_coupling, c->xchg, c->gx, c->update_split, c->err, &c->upd_epoch);
+                      c->cfg.leg_coupling, c->xchg, c->gx, c->update_split, c->err, &c->upd_epoch, c->xchg_coherent);
   else if (c->pol[0].last_steps > 0) {   // one shared policy
     const int last = c->pol[0].last_steps;
     launch_gnn_schedule(c->stream, ua[0], last, 0, c->gnn);
@@ -676,7 +683,7 @@ int ddrl_ppo_grad(ddrl_ctx* c, int pid, const int32_t* rows, int n_rows, float k
   if (c->cfg.model_kind == DDRL_MODEL_FFN)
     launch_update_ffn(c->stream, &u, h, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim,
                       c->pol[pid].d, c->pol[pid].lay.stride, c->cfg.leg_coupling, c->xchg, c->gx,
-                      grad_split(c, n_rows), c->err, &c->upd_epoch);
+                      grad_split(c, n_rows), c->err, &c->upd_epoch, c->xchg_coherent);
   else
     launch_step_gnn(c->stream, u, h, 0, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->gnn);
   HIPCHK(hipGetLastError());
@@ -749,7 +756,7 @@ int ddrl_ppo_update_ddp(ddrl_ctx* c, int pid, const int32_t* shuffle, const int3
   for (int s = 0; s < steps; ++s) {
     if (ffn)
       launch_update_ffn(c->stream, &ua[s], h, m, inv_n, c->cfg.act_dim, P.d, P.lay.stride, c->cfg.leg_coupling,
-                        c->xchg, c->gx, grad_split(c, m), c->err, &c->upd_epoch);
+                        c->xchg, c->gx, grad_split(c, m), c->err, &c->upd_epoch, c->xchg_coherent);
     else
       launch_step_gnn(c->stream, ua[s], h, 0, m, inv_n, c->gnn);
     NCCLCHK(ncclAllReduce(P.grad, P.grad, (size_t)P.n_params, ncclFloat32, ncclSum, c->comm, c->stream));

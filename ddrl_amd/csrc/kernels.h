@@ -132,7 +132,8 @@ struct UpdateHyper {
 // d / stride: the widest obs width / record stride of the launched policies
 void launch_update_ffn(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n, int A, int d,
                        int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp, int* err,
-                       unsigned* epoch_ctr);   // per-context launch counter (granule tags)
+                       unsigned* epoch_ctr,    // per-context launch counter (granule tags)
+                       int coherent);          // 1: device-coherent exchange stores (any placement)
 size_t gx_bytes(int P);
 // clip_by_global_norm + tf1 Adam on a flat (all-reduced) gradient vector
 // gscale multiplies the gradient before the clip (1 / ranks in the "local" data-parallel mode)

@@ -58,6 +58,7 @@ struct UpdateBatch {
   int* err;              // set to 1 if an exchange timed out
   unsigned epoch;        // launch counter (12 bits, never 0): high bits of every exchange tag
   unsigned lds_bytes;    // dynamic LDS of the launch (bounds-checked build)
+  int coherent;          // 1: exchange stores are sc1 (any workgroup placement), see gx_put
 };
 
 // Bounds-checked diagnostic build (-DDDRL_BOUNDS, tools/build_diag.py): every staging,
@@ -369,19 +370,74 @@ __device__ __forceinline__ bool xchg_abandon(unsigned long long t0, int* err) {
   if (dt > XCHG_TIMEOUT_TICKS) { atomicExch(err, 1); return true; }
   return false;
 }
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t gx_rsrc(unsigned long long* box) {
+// Two builds of the same protocol:
+//  * default: plain stores into the XCD's shared L2 and sc1 polls (0.24 us per hop); correct
+//    when the workgroups that exchange share an L2, which every workgroup verifies at entry
+//    (its XCC id must be its policy's, block & 7: the dispatcher's round robin).  A misplaced
+//    workgroup raises error 2 and leaves; the launch option `coherent` (DDRL_XCHG_COHERENT=1)
+//    makes the stores sc1 (device-coherent write-through: the ISA of a relaxed agent-scope
+//    atomic store), valid for any placement, 0.50 us per hop.
+//  * -DDDRL_XCHG_ATOMIC: every granule access is a relaxed agent-scope 64-bit atomic
+//    (__hip_atomic_load / __hip_atomic_store): defined behaviour under the HIP memory model
+//    for any placement, each 8-byte {value, tag} half its own atomic.  The bounds-checked
+//    diagnostic library is built this way, so the GPU suite runs the update under both.
+#ifdef DDRL_XCHG_ATOMIC
+typedef unsigned long long* gx_box_t;
+__device__ __forceinline__ gx_box_t gx_rsrc(unsigned long long* box) { return box; }
+__device__ __forceinline__ void gx_put(gx_box_t r, int j, float v0, float v1, unsigned tag, bool) {
+  unsigned long long* g = r + 2 * (j * 256 + (int)threadIdx.x);
+  __hip_atomic_store(g, ((unsigned long long)tag << 32) | __float_as_uint(v0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(g + 1, ((unsigned long long)tag << 32) | __float_as_uint(v1), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void xchg_store(unsigned long long* g, unsigned long long v, bool) {
+  __hip_atomic_store(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long xchg_load(unsigned long long* g) {
+  return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <int NP>
+__device__ __forceinline__ void gx_get(gx_box_t r, unsigned tag, float* out, int* err) {
+  unsigned long long g[2 * NP];
+  unsigned long long* b = r + 2 * (int)threadIdx.x;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      g[2 * j] = __hip_atomic_load(b + 512 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      g[2 * j + 1] = __hip_atomic_load(b + 512 * j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 2 * NP; ++j) ok = ok && (unsigned)(g[j] >> 32) == tag;
+    if (ok) break;
+    if (xchg_abandon(t0, err)) {
+#pragma unroll
+      for (int j = 0; j < 2 * NP; ++j) g[j] = 0ull;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+#pragma unroll
+  for (int j = 0; j < 2 * NP; ++j) out[j] = __uint_as_float((unsigned)g[j]);
+}
+#else
+typedef __amdgpu_buffer_rsrc_t gx_box_t;
+__device__ __forceinline__ gx_box_t gx_rsrc(unsigned long long* box) {
   return __builtin_amdgcn_make_buffer_rsrc(box, 0, GX_MAX_PAIRS * 256 * 16, 0x00020000);
 }
-__device__ __forceinline__ void gx_put(__amdgpu_buffer_rsrc_t r, int j, float v0, float v1, unsigned tag) {
+__device__ __forceinline__ void gx_put(gx_box_t r, int j, float v0, float v1, unsigned tag, bool coh) {
   const v4u g = {__float_as_uint(v0), tag, __float_as_uint(v1), tag};
-  __builtin_amdgcn_raw_buffer_store_b128(g, r, (j * 256 + (int)threadIdx.x) * 16, 0, DDRL_GX_ST);
+  if (coh) __builtin_amdgcn_raw_buffer_store_b128(g, r, (j * 256 + (int)threadIdx.x) * 16, 0, 16);
+  else __builtin_amdgcn_raw_buffer_store_b128(g, r, (j * 256 + (int)threadIdx.x) * 16, 0, DDRL_GX_ST);
 }
 // Norm granule (8 bytes: tag << 32 | value), one 64-bit access each way, same policy.
-__device__ __forceinline__ void xchg_store(unsigned long long* g, unsigned long long v) {
+__device__ __forceinline__ void xchg_store(unsigned long long* g, unsigned long long v, bool coh) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(g, 0, 8, 0x00020000);
   typedef unsigned v2u_t __attribute__((ext_vector_type(2)));
   const v2u_t x = {(unsigned)v, (unsigned)(v >> 32)};
-  __builtin_amdgcn_raw_buffer_store_b64(x, r, 0, 0, DDRL_GX_ST);
+  if (coh) __builtin_amdgcn_raw_buffer_store_b64(x, r, 0, 0, 16);
+  else __builtin_amdgcn_raw_buffer_store_b64(x, r, 0, 0, DDRL_GX_ST);
 }
 __device__ __forceinline__ unsigned long long xchg_load(unsigned long long* g) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(g, 0, 8, 0x00020000);
@@ -393,7 +449,7 @@ __device__ __forceinline__ unsigned long long xchg_load(unsigned long long* g) {
 // The partner's NP pairs of this lane: all loads in flight, re-polled until every tag
 // matches; bounded (a timeout flags err and returns zeros).
 template <int NP>
-__device__ __forceinline__ void gx_get(__amdgpu_buffer_rsrc_t r, unsigned tag, float* out, int* err) {
+__device__ __forceinline__ void gx_get(gx_box_t r, unsigned tag, float* out, int* err) {
   v4u g[NP];
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
@@ -417,6 +473,7 @@ __device__ __forceinline__ void gx_get(__amdgpu_buffer_rsrc_t r, unsigned tag, f
     out[2 * j + 1] = __uint_as_float(g[j][2]);
   }
 }
+#endif
 
 template <int A, int KS1, int OB, bool POL, int NW, int KSP, bool CUP>
 __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBatch& ub, float* lds, int p, int kq) {
@@ -450,6 +507,17 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   const int stride = U.lay.stride, cpr = stride >> 2, cpr_l = stg_chunks(stride, A);
 
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, q = lane >> 4, w = tid >> 6;
+  const bool coh = ub.coherent != 0;
+#ifndef DDRL_XCHG_ATOMIC
+  if (!coh) {   // the L2 protocol needs every workgroup of this policy on XCD p (see gx_put)
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    if ((xcc & 7u) != (unsigned)p) {
+      if (tid == 0) atomicExch(ub.err, 2);   // the partners see it at their first slow wait
+      return;
+    }
+  }
+#endif
   int row_l[RT];
   bool row_ok[RT];
 #pragma unroll
@@ -660,7 +728,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     STAMP(5);
     const unsigned gtag = xchg_tag(ub.epoch, step);
     const size_t gx_box = (size_t)GX_MAX_PAIRS * 256 * 2;   // granules per outbox
-    const __amdgpu_buffer_rsrc_t gx_mine = gx_rsrc(ub.gx + ((gx_branch + kq) * 2 + (step & 1)) * gx_box);
+    const gx_box_t gx_mine = gx_rsrc(ub.gx + ((gx_branch + kq) * 2 + (step & 1)) * gx_box);
     float gs[NSLOT];
     float st_own = 0.f;
     if constexpr (KSP == 2) {
@@ -681,7 +749,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
         for (int i = 0; i < NW; ++i) st_own += red[i * 8 + tid];
       v0[NSLOT] = st_own;
 #pragma unroll
-      for (int j = 0; j < NP0; ++j) gx_put(gx_mine, j, v0[2 * j], v0[2 * j + 1], gtag);
+      for (int j = 0; j < NP0; ++j) gx_put(gx_mine, j, v0[2 * j], v0[2 * j + 1], gtag, coh);
     }
     floatx4 gt[NTS];
 #ifndef DDRL_ABL_NO_DW2   // ablation builds (timing only): skip a phase
@@ -692,8 +760,8 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     if constexpr (KSP == 2) {
 #pragma unroll
       for (int i = 0; i < NS1; ++i) {
-        gx_put(gx_mine, NP0 + 2 * i, gt[i][0], gt[i][1], gtag);
-        gx_put(gx_mine, NP0 + 2 * i + 1, gt[i][2], gt[i][3], gtag);
+        gx_put(gx_mine, NP0 + 2 * i, gt[i][0], gt[i][1], gtag, coh);
+        gx_put(gx_mine, NP0 + 2 * i + 1, gt[i][2], gt[i][3], gtag, coh);
       }
     }
     STAMP(6);
@@ -744,8 +812,8 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       // both workgroups hold the same bits)
 #pragma unroll
       for (int i = NS1; i < NTS; ++i) {
-        gx_put(gx_mine, NP0 + 2 * i, gt[i][0], gt[i][1], gtag);
-        gx_put(gx_mine, NP0 + 2 * i + 1, gt[i][2], gt[i][3], gtag);
+        gx_put(gx_mine, NP0 + 2 * i, gt[i][0], gt[i][1], gtag, coh);
+        gx_put(gx_mine, NP0 + 2 * i + 1, gt[i][2], gt[i][3], gtag, coh);
       }
       float o[2 * NP];
       gx_get<NP>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), gtag, o, ub.err);
@@ -810,7 +878,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       float local = 0.f;
       for (int i = 0; i < NW; ++i) local += red[64 + i];
       const unsigned tag = xchg_tag(ub.epoch, step);
-      xchg_store(xmine, ((unsigned long long)tag << 32) | __float_as_uint(local));
+      xchg_store(xmine, ((unsigned long long)tag << 32) | __float_as_uint(local), coh);
       unsigned long long v = xv;
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 #ifdef DDRL_ABL_NO_EXCHANGE
@@ -967,8 +1035,9 @@ static void launch_update_t(hipStream_t s, UpdateBatch& ub, int P, int stride, i
 
 void launch_update_ffn(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n,
                        int A, int d, int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp,
-                       int* err, unsigned* epoch_ctr) {
+                       int* err, unsigned* epoch_ctr, int coherent) {
   UpdateBatch ub;
+  ub.coherent = coherent;
   for (int p = 0; p < DDRL_MAXP; ++p) ub.a[p] = p < h.P ? ua[p] : UpdateArgs{};
   ub.h = h;
   ub.nrows = nrows;

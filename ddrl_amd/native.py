@@ -119,9 +119,13 @@ def comm_unique_id():
 
 
 def load(path: str = LIB_PATH):
+    """The HIP library.  DDRL_LIB names an alternative in-tree build of the same ABI (the
+    diagnostic variants of ddrl_amd/build.py, e.g. libddrl_hip_atomic.so) for A/B timing."""
     global _lib
     if _lib is not None:
         return _lib
+    if path == LIB_PATH and os.environ.get("DDRL_LIB"):
+        path = os.path.join(HERE, os.path.basename(os.environ["DDRL_LIB"]))
     if not os.path.exists(path):
         raise DdrlError(f"{path} is missing: build it with `python -m ddrl_amd.build` "
                         "(the HIP library is the only compute path; there is no fallback)")
