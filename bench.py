@@ -219,34 +219,24 @@ def main():
 
     ctx.observe(syn.obs[0])
 
-    host = None
+    henv = None
+    host_threads = int(os.environ.get("OMP_NUM_THREADS") or min(16, os.cpu_count() or 1))
 
-    def rollout_host_io(done):
-        """The rollout through pinned host buffers (ddrl_act_host / ddrl_env_step_host), the
-        interface of a host-side env plane: every env step waits for its actions on the host
-        (the envs step there) before the env's answer goes back (PCIe both ways each step).
-        The envs' data cycles through a 4-slot pinned ring (contents do not matter here)."""
-        nonlocal host
-        if host is None:
-            pin = lambda x: x[:4].cpu().contiguous().pin_memory()
-            host = dict(obs=pin(syn.obs), eps=pin(syn.eps), fw=pin(syn.fw), cfrc=pin(syn.cfrc),
-                        act=torch.zeros((n_local, 8), dtype=torch.float32).pin_memory(),
-                        done=torch.zeros((4, n_local), dtype=torch.uint8).pin_memory())
-        host["done"].copy_(done[:4].cpu())
-        for t in range(T):
-            s = t % 4
-            if t == 0:
-                ctx.step_host(0, host["obs"][0], host["eps"][0], host["act"])
-            else:
-                ctx.act_host(t, host["eps"][s], host["act"])
-            stream.synchronize()
-            ctx.env_step_host(t, host["fw"][s], host["cfrc"][s], host["done"][s], host["obs"][(t + 1) % 4])
+    def rollout_host_env(groups=2):
+        """The rollout with the envs stepped on the host (f1): the C++ thread pool steps the
+        QuAntruped stand-in into pinned buffers, pipelined over env groups so that one
+        group's host step overlaps the device's reward / observe / act of the other and the
+        PCIe transfers (ddrl_rollout_hostenv).  The first call resets the envs."""
+        nonlocal henv
+        first = henv is None
+        if first:
+            henv = N.HostEnv(n_local, cfg.obs_full_dim, host_threads, seed=1000 + rank)
+        ctx.rollout_hostenv(henv, syn.eps, groups=groups, reset=first)
 
     def iteration(record, host_io=False):
         done = syn.dones_for_fragment()
         if host_io:
-            rollout_host_io(done)
-            ctx.bootstrap()
+            rollout_host_env()
         else:
             # T x (act, reward, observe) + bootstrap in one C-ABI call (device-resident env data)
             ctx.rollout_fragment(syn.obs, syn.eps, syn.fw, syn.cfrc, done, syn.actions)
@@ -319,24 +309,38 @@ def main():
 
     pcie = None
     if world == 1 and not args.no_pcie and not ddp:
-        # one more iteration with the rollout through pinned host buffers (not part of value)
+        # one more iteration with the envs on the host (not part of value): pipelined host env
+        # plane rollout + GAE + the same update
+        torch.cuda.synchronize()
+        rollout_host_env()            # warm-up: resets the envs, first pinned transfers
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         iteration(False, host_io=True)
         torch.cuda.synchronize()
         it_s = time.perf_counter() - t1
-        torch.cuda.synchronize()
-        t2 = time.perf_counter()
-        rollout_host_io(syn.dones_for_fragment())
-        torch.cuda.synchronize()
-        ro_s = time.perf_counter() - t2
-        per_step_bytes = 4 * n_local * (cfg.obs_full_dim + cfg.n_agents * A + 8 + 1 + 14 * 6) + n_local
+        ro = {}
+        for groups in (1, 2):
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            rollout_host_env(groups)
+            torch.cuda.synchronize()
+            ro[groups] = time.perf_counter() - t2
+        t3 = time.perf_counter()
+        for _ in range(20):
+            henv.step()
+        step_s = (time.perf_counter() - t3) / 20
+        per_step_bytes = 4 * n_local * (cfg.obs_full_dim + 8 + 1 + 14 * 6) + n_local
         pcie = {"value": T * n_local / it_s, "unit": "env-steps/s", "iteration_ms": it_s * 1e3,
-                "rollout_ms": ro_s * 1e3, "rollout_env_steps_per_s": T * n_local / ro_s,
+                "rollout_ms": ro[2] * 1e3, "rollout_env_steps_per_s": T * n_local / ro[2],
+                "rollout_ms_unpipelined": ro[1] * 1e3, "host_env_step_ms": step_s * 1e3,
+                "host_threads": henv.threads, "env_groups": 2,
                 "pcie_bytes_per_vector_step": per_step_bytes,
-                "note": "one iteration with the rollout through pinned host buffers "
-                        "(ddrl_step_host / ddrl_act_host / ddrl_env_step_host), a host sync per env "
-                        "step for the host env plane; the env stepping itself is not included"}
+                "note": "one iteration with the envs stepped on the host: the C++ thread pool steps the "
+                        "clean-room QuAntruped stand-in (not MuJoCo) into pinned buffers, pipelined over 2 env "
+                        "groups (ddrl_rollout_hostenv: one group's host step overlaps the other's device work "
+                        "and PCIe transfers); rollout_ms_unpipelined = the same with one group; host_env_step_ms "
+                        "= one host step of all envs alone"}
+        henv.close()
 
     upd_avg_ms = float(np.mean(upd_ms))
     steps_per_policy = int(steps_done[-1])

@@ -74,7 +74,7 @@ def _build(force, verbose, extra_flags):
     with ThreadPoolExecutor(max_workers=n) as ex:
         list(ex.map(run, jobs))
     if jobs or force or _stale(LIB, objs):
-        run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs, "-L/opt/rocm/lib", "-lrccl"])
+        run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs, "-L/opt/rocm/lib", "-lrccl", "-lpthread"])
     return LIB
 
 
@@ -89,15 +89,29 @@ def build_bounds(force: bool = False, verbose: bool = False) -> str:
                  build_dir=os.path.join(HERE, "_build_bounds"))
 
 
+ATOMIC_LIB = os.path.join(HERE, "libddrl_hip_atomic.so")
+
+
+def build_atomic(force: bool = False, verbose: bool = False) -> str:
+    """The production kernels with the exchange granules as relaxed agent-scope atomics
+    (-DDDRL_XCHG_ATOMIC: valid for any workgroup placement, 1.1 us per step slower); load it
+    with DDRL_LIB=libddrl_hip_atomic.so."""
+    return build(force, verbose, extra_flags=["-DDDRL_XCHG_ATOMIC"], lib=ATOMIC_LIB,
+                 build_dir=os.path.join(HERE, "_build_atomic"))
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("--bounds", action="store_true", help="also build libddrl_hip_bounds.so")
+    ap.add_argument("--atomic", action="store_true", help="also build libddrl_hip_atomic.so")
     a = ap.parse_args(argv)
     print(build(a.force, a.verbose))
     if a.bounds:
         print(build_bounds(a.force, a.verbose))
+    if a.atomic:
+        print(build_atomic(a.force, a.verbose))
 
 
 if __name__ == "__main__":

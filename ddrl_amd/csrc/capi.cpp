@@ -12,6 +12,7 @@
 #include <rccl/rccl.h>
 
 #include "../../include/ddrl_hip.h"
+#include "hostenv.h"
 #include "kernels.h"
 
 namespace {
@@ -70,7 +71,6 @@ struct ddrl_ctx {
   unsigned long long* gx = nullptr;    // partial-gradient granules of the row-split update
   unsigned upd_epoch = 0;              // update launches so far (granule tag epochs)
   int update_split = 2;                // workgroups per branch of the fused update (1 or 2)
-  int xchg_coherent = 0;               // 1: device-coherent exchange stores (DDRL_XCHG_COHERENT=1)
   int* err = nullptr;                  // device error word (exchange timeout)
   float kl_last[DDRL_MAXP] = {0};
   GnnScratch gnn{};               // GraphNet step scratch (per-tile partial gradients, ...)
@@ -167,9 +167,6 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
   ddrl_ctx* c = new ddrl_ctx();
   // fused update geometry: DDRL_UPDATE_SPLIT=1 keeps one workgroup per branch (timing / A-B)
   if (const char* e = std::getenv("DDRL_UPDATE_SPLIT")) c->update_split = std::atoi(e) == 1 ? 1 : 2;
-  // exchange protocol of the fused update: the XCD-local L2 protocol by default (every
-  // workgroup checks its placement), device-coherent stores with DDRL_XCHG_COHERENT=1
-  if (const char* e = std::getenv("DDRL_XCHG_COHERENT")) c->xchg_coherent = std::atoi(e) == 1;
   c->cfg = *cfg;
   c->device = device;
   const ddrl_cfg& g = c->cfg;
@@ -275,7 +272,8 @@ static int check_err(ddrl_ctx* c) {
     (void)hipMemset(c->err, 0, sizeof(int));
     if (e == 2)
       return fail("update kernel: a workgroup was not placed on its policy's XCD, so the XCD-local exchange "
-                  "protocol cannot run (rerun with DDRL_XCHG_COHERENT=1: device-coherent exchange stores)");
+                  "protocol cannot run (build the atomic-exchange library, `python -m ddrl_amd.build --atomic`, "
+                  "and run with DDRL_LIB=libddrl_hip_atomic.so)");
     return fail("update kernel: norm exchange between the policy and value workgroups timed out");
   }
   return 0;
@@ -434,23 +432,39 @@ int ddrl_adv_sums_get(ddrl_ctx* c, int pid, double* host3) {
   return 0;
 }
 
-int ddrl_observe(ddrl_ctx* c, const float* obs) {
+static int check_range(const ddrl_ctx* c, int e0, int e1) {
+  if (e0 < 0 || e1 > c->cfg.n_envs || e0 >= e1) return fail("env range [e0, e1) must lie in [0, n_envs) and be non-empty");
+  return 0;
+}
+
+// observe / act / reward over the envs [e0, e1) (the whole shard, or one group of a
+// pipelined host env plane): the env-side filter pushes the range's rows as one batch.
+int ddrl_observe_range(ddrl_ctx* c, const float* obs, int e0, int e1) {
   CHK_CTX(c);
   if (!obs) return fail("null observation buffer");
+  if (check_range(c, e0, e1)) return -1;
   const ddrl_cfg& g = c->cfg;
-  launch_filter_push(c->stream, obs, g.n_envs, g.obs_full_dim, c->f_n, c->f_M, c->f_S, c->f_normc,
+  const int n = e1 - e0;
+  const float* obs_r = obs + (size_t)e0 * g.obs_full_dim;
+  RouteArgs ra = c->route;
+  ra.N = n;
+  ra.e0 = e0;
+  launch_filter_push(c->stream, obs_r, n, g.obs_full_dim, c->f_n, c->f_M, c->f_S, c->f_normc,
                      g.filter_update, g.filter_enabled, c->f_dn, c->f_dM, c->f_dS);
   const float clip = g.filter_enabled ? g.filter_clip : 0.f;
-  if (g.policy_filter) launch_policy_filter(c->stream, c->route, obs, c->f_normc, clip, c->zs, c->pf, 1);
-  const FilterCount fc{c->f_n, c->f_dn, g.filter_enabled && g.filter_update ? g.n_envs : 0};
+  if (g.policy_filter) launch_policy_filter(c->stream, ra, obs_r, c->f_normc, clip, c->zs, c->pf, 1);
+  const FilterCount fc{c->f_n, c->f_dn, g.filter_enabled && g.filter_update ? n : 0};
   if (g.model_kind == DDRL_MODEL_FFN)
-    launch_observe_ffn(c->stream, c->route, obs, c->f_normc, clip, c->stage_tab, g.policy_filter ? c->pf : nullptr,
-                       fc);
+    launch_observe_ffn(c->stream, ra, obs, c->f_normc, clip, c->stage_tab, g.policy_filter ? c->pf : nullptr, fc);
   else
-    launch_observe_gnn(c->stream, c->route, obs, c->f_normc, g.filter_enabled ? g.filter_clip : 0.f,
-                       c->pol[0].stage, fc);
+    launch_observe_gnn(c->stream, ra, obs, c->f_normc, g.filter_enabled ? g.filter_clip : 0.f, c->pol[0].stage, fc);
   HIPCHK(hipGetLastError());
   return 0;
+}
+
+int ddrl_observe(ddrl_ctx* c, const float* obs) {
+  CHK_CTX(c);
+  return ddrl_observe_range(c, obs, 0, c->cfg.n_envs);
 }
 
 static ActArgs make_act(ddrl_ctx* c, int t, const float* eps, float* actions, int mode) {
@@ -462,6 +476,7 @@ static ActArgs make_act(ddrl_ctx* c, int t, const float* eps, float* actions, in
     aa.cup[p] = c->cfg.leg_coupling ? P.theta + ffn_param_count(P.d, c->cfg.act_dim) : nullptr;
   }
   aa.t = t; aa.eps = eps; aa.actions = actions; aa.bootstrap = mode;
+  aa.e0 = 0; aa.e1 = c->cfg.n_envs;
   return aa;
 }
 
@@ -479,6 +494,17 @@ int ddrl_act(ddrl_ctx* c, int t, const float* eps, float* actions) {
   return launch_act(c, make_act(c, t, eps, actions, 0));
 }
 
+int ddrl_act_range(ddrl_ctx* c, int t, int e0, int e1, const float* eps, float* actions) {
+  CHK_CTX(c);
+  if (t < 0 || t >= c->cfg.frag_len) return fail("t out of range");
+  if (!eps || !actions) return fail("null eps/actions buffer");
+  if (check_range(c, e0, e1)) return -1;
+  ActArgs aa = make_act(c, t, eps, actions, 0);
+  aa.e0 = e0;
+  aa.e1 = e1;
+  return launch_act(c, aa);
+}
+
 int ddrl_bootstrap(ddrl_ctx* c) {
   CHK_CTX(c);
   return launch_act(c, make_act(c, 0, nullptr, nullptr, 1));
@@ -487,11 +513,19 @@ int ddrl_bootstrap(ddrl_ctx* c) {
 int ddrl_reward(ddrl_ctx* c, int t, const float* fw, const float* cfrc, const float* actions,
                 const uint8_t* done) {
   CHK_CTX(c);
+  return ddrl_reward_range(c, t, 0, c->cfg.n_envs, fw, cfrc, actions, done);
+}
+
+int ddrl_reward_range(ddrl_ctx* c, int t, int e0, int e1, const float* fw, const float* cfrc, const float* actions,
+                      const uint8_t* done) {
+  CHK_CTX(c);
   if (t < 0 || t >= c->cfg.frag_len) return fail("t out of range");
   if (!fw || !cfrc || !actions) return fail("null reward input");
+  if (check_range(c, e0, e1)) return -1;
   const ddrl_cfg& g = c->cfg;
   RewardArgs ra{};
   ra.P = g.n_policies; ra.N = g.n_envs; ra.n_agents = g.n_agents; ra.mode = g.reward_mode;
+  ra.e0 = e0; ra.n = e1 - e0;
   ra.ctrl_w = g.ctrl_cost_weight; ra.contact_w = g.contact_cost_weight; ra.t = t;
   for (int p = 0; p < g.n_policies; ++p) {
     ra.k[p] = c->pol[p].k; ra.rec[p] = c->pol[p].rec; ra.lay[p] = c->pol[p].lay;
@@ -567,6 +601,69 @@ int ddrl_env_step_host(ddrl_ctx* c, int t, const float* fw_h, const float* cfrc_
   return ddrl_observe(c, c->h_obs);
 }
 
+// f1: a fragment with the envs stepped on the host (ddrl_hostenv, hostenv.cpp), pipelined over
+// `groups` env groups: while the host threads step group g, the device runs the other groups'
+// reward / observe / act and the transfers.  Per step t and group g (envs [e0, e1)):
+//   wait for the actions of (t, g) (event) -> host step of [e0, e1) into the pinned buffers ->
+//   H2D of the group's fw / cfrc / done / next obs -> reward_range(t) -> observe_range ->
+//   act_range(t + 1) -> D2H of the group's actions -> event.
+// The call order on the stream is the same as a synchronous loop over the same groups, so the
+// records are bit-identical to it (tests/test_gpu_hostenv.py).  reset: 1 = reset every env
+// first and observe the reset observations (per group); 0 = continue from the observation
+// the context holds.  eps_dev: [T][N][n_agents][A] exploration noise in HBM.  Ends with the
+// bootstrap V(s_T) of every env.
+int ddrl_rollout_hostenv(ddrl_ctx* c, ddrl_hostenv* env, int groups, const float* eps_dev, int reset) {
+  CHK_CTX(c);
+  const ddrl_cfg& g = c->cfg;
+  if (!env || !eps_dev) return fail("null host env / noise buffer");
+  if (env->N != g.n_envs || env->D != g.obs_full_dim) return fail("host env shape differs from the context's");
+  if (groups < 1 || groups > 8 || groups > g.n_envs) return fail("groups must be in [1, min(8, n_envs)]");
+  const int N = g.n_envs, D = g.obs_full_dim, T = g.frag_len;
+  const size_t eps_step = (size_t)N * g.n_agents * g.act_dim;
+  std::vector<int> lo(groups + 1);
+  for (int k = 0; k <= groups; ++k) lo[k] = (int)((long long)N * k / groups);
+  std::vector<hipEvent_t> ev(groups, nullptr);
+  for (auto& e : ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  int rc = 0;
+  auto h2d = [&](void* dst, const void* src, size_t bytes) {
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream) == hipSuccess ? 0 : fail("H2D copy failed");
+  };
+  auto d2h_act = [&](int k) {
+    const size_t off = (size_t)lo[k] * 8;
+    if (hipMemcpyAsync(env->act + off, c->h_act + off, (size_t)(lo[k + 1] - lo[k]) * 8 * 4, hipMemcpyDeviceToHost,
+                       c->stream) != hipSuccess || hipEventRecord(ev[k], c->stream) != hipSuccess)
+      return fail("D2H copy failed");
+    return 0;
+  };
+  if (reset) env->reset_all();
+  for (int k = 0; k < groups && !rc; ++k) {
+    const int e0 = lo[k], e1 = lo[k + 1];
+    if (reset) rc = h2d(c->h_obs + (size_t)e0 * D, env->obs + (size_t)e0 * D, (size_t)(e1 - e0) * D * 4) ||
+                    ddrl_observe_range(c, c->h_obs, e0, e1);
+    rc = rc || ddrl_act_range(c, 0, e0, e1, eps_dev, c->h_act) || d2h_act(k);
+  }
+  for (int t = 0; t < T && !rc; ++t) {
+    for (int k = 0; k < groups && !rc; ++k) {
+      const int e0 = lo[k], e1 = lo[k + 1], n = e1 - e0;
+      if (hipEventSynchronize(ev[k]) != hipSuccess) { rc = fail("event wait failed"); break; }
+      env->step(e0, e1);   // host threads; the device meanwhile runs the other groups' work
+      rc = h2d(c->h_fw + e0, env->fw + e0, (size_t)n * 4) ||
+           h2d(c->h_cfrc + (size_t)e0 * 84, env->cfrc + (size_t)e0 * 84, (size_t)n * 84 * 4) ||
+           h2d(c->h_done + e0, env->done + e0, (size_t)n) ||
+           h2d(c->h_obs + (size_t)e0 * D, env->obs + (size_t)e0 * D, (size_t)n * D * 4) ||
+           ddrl_reward_range(c, t, e0, e1, c->h_fw, c->h_cfrc, c->h_act, c->h_done) ||
+           ddrl_observe_range(c, c->h_obs, e0, e1);
+      if (!rc && t + 1 < T)
+        rc = ddrl_act_range(c, t + 1, e0, e1, eps_dev + (size_t)(t + 1) * eps_step, c->h_act) || d2h_act(k);
+    }
+  }
+  if (!rc) rc = ddrl_bootstrap(c);
+  // the pinned buffers are the caller's again only once the stream has consumed them
+  if (hipStreamSynchronize(c->stream) != hipSuccess && !rc) rc = fail("stream synchronize failed");
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  return rc ? -1 : 0;
+}
+
 int ddrl_gae(ddrl_ctx* c) {
   CHK_CTX(c);
   const ddrl_cfg& g = c->cfg;
@@ -632,7 +729,7 @@ int ddrl_ppo_update(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const 
   // the arguments travel by value in the kernel's argument block (no copy from this stack frame)
   if (c->cfg.model_kind == DDRL_MODEL_FFN)
     launch_update_ffn(c->stream, ua, h, 128, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim, maxd, maxs,
-                      c->cfg.leg_coupling, c->xchg, c->gx, c->update_split, c->err, &c->upd_epoch, c->xchg_coherent);
+                      c->cfg.leg_coupling, c->xchg, c->gx, c->update_split, c->err, &c->upd_epoch);
   else if (c->pol[0].last_steps > 0) {   // one shared policy
     const int last = c->pol[0].last_steps;
     launch_gnn_schedule(c->stream, ua[0], last, 0, c->gnn);
@@ -683,7 +780,7 @@ int ddrl_ppo_grad(ddrl_ctx* c, int pid, const int32_t* rows, int n_rows, float k
   if (c->cfg.model_kind == DDRL_MODEL_FFN)
     launch_update_ffn(c->stream, &u, h, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim,
                       c->pol[pid].d, c->pol[pid].lay.stride, c->cfg.leg_coupling, c->xchg, c->gx,
-                      grad_split(c, n_rows), c->err, &c->upd_epoch, c->xchg_coherent);
+                      grad_split(c, n_rows), c->err, &c->upd_epoch);
   else
     launch_step_gnn(c->stream, u, h, 0, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->gnn);
   HIPCHK(hipGetLastError());
@@ -756,7 +853,7 @@ int ddrl_ppo_update_ddp(ddrl_ctx* c, int pid, const int32_t* shuffle, const int3
   for (int s = 0; s < steps; ++s) {
     if (ffn)
       launch_update_ffn(c->stream, &ua[s], h, m, inv_n, c->cfg.act_dim, P.d, P.lay.stride, c->cfg.leg_coupling,
-                        c->xchg, c->gx, grad_split(c, m), c->err, &c->upd_epoch, c->xchg_coherent);
+                        c->xchg, c->gx, grad_split(c, m), c->err, &c->upd_epoch);
     else
       launch_step_gnn(c->stream, ua[s], h, 0, m, inv_n, c->gnn);
     NCCLCHK(ncclAllReduce(P.grad, P.grad, (size_t)P.n_params, ncclFloat32, ncclSum, c->comm, c->stream));

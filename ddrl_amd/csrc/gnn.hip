@@ -90,7 +90,7 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
   int sel = 0;
   int ridx = 0;
   if constexpr (MODE == GNN_ACT) {
-    X = ga.x + (size_t)(gvalid ? graph : 0) * 92;
+    X = ga.x + (size_t)(ga.act_e0 + (gvalid ? graph : 0)) * 92;
   } else if constexpr (MODE == GNN_FWD) {
     X = ga.x + (size_t)(gvalid ? graph : 0) * 92;
     sel = gvalid ? ga.node[graph] : 0;
@@ -209,14 +209,14 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
 
   if constexpr (MODE == GNN_ACT) {
     if (tid < 16) {
-      const int cc = tid, gg = cc >> 2, nn = cc & 3, e = 4 * tile + gg;
-      if (e < ga.n_graphs) {
+      const int cc = tid, gg = cc >> 2, nn = cc & 3, el = 4 * tile + gg, e = ga.act_e0 + el;
+      if (el < ga.n_graphs) {
         float out[O];
 #pragma unroll
         for (int o = 0; o < O; ++o)
           out[o] = (((hp[cc * 4 + o] + hp[(16 + cc) * 4 + o]) + hp[(32 + cc) * 4 + o]) +
                     hp[(48 + cc) * 4 + o]) + th[off.bout + o];
-        const int C = 4 * ga.n_graphs;
+        const int C = 4 * ga.act_nfull;
         const int row = e * 4 + nn;
         if (NET == 1) {
           if (ga.bootstrap) ga.last_v[row] = out[0];
@@ -243,10 +243,10 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
     }
     if (NET == 0 && !ga.bootstrap) {
       // graph observation + node index into the 16 records of the tile
-      const int C = 4 * ga.n_graphs;
+      const int C = 4 * ga.act_nfull;
       for (int idx = tid; idx < 16 * 93; idx += 256) {
-        const int rr = idx / 93, f = idx - rr * 93, e = 4 * tile + (rr >> 2);
-        if (e >= ga.n_graphs) continue;
+        const int rr = idx / 93, f = idx - rr * 93, el = 4 * tile + (rr >> 2), e = ga.act_e0 + el;
+        if (el >= ga.n_graphs) continue;
         const float v = f < 92 ? ga.x[(size_t)e * 92 + f] : (float)(rr & 3);
         ga.rec[((size_t)ga.t * C + e * 4 + (rr & 3)) * ga.lay.stride + ga.lay.obs + f] = v;
       }
@@ -607,13 +607,15 @@ void launch_act_gnn(hipStream_t s, const RouteArgs& ra, const ActArgs& aa) {
   check_a(ra.A);
   GnnArgs ga{};
   ga.theta = aa.theta[0];
-  ga.n_graphs = ra.N;
+  ga.n_graphs = aa.e1 - aa.e0;   // the env range [e0, e1) of this call
+  ga.act_e0 = aa.e0;
+  ga.act_nfull = ra.N;
   ga.x = aa.stage[0];
   ga.rec = aa.rec[0]; ga.lay = aa.lay[0]; ga.t = aa.t; ga.eps = aa.eps; ga.actions = aa.actions;
   ga.n_agents = ra.n_agents; ga.bootstrap = aa.bootstrap; ga.last_v = aa.last_v[0];
   for (int a = 0; a < 4; ++a)
     for (int j = 0; j < 8; ++j) ga.act_index[a][j] = ra.pol[0].act_index[a][j];
-  hipLaunchKernelGGL((k_gnn<2, GNN_ACT>), dim3((ra.N + 3) / 4, 2), dim3(256), 0, s, ga);
+  hipLaunchKernelGGL((k_gnn<2, GNN_ACT>), dim3((ga.n_graphs + 3) / 4, 2), dim3(256), 0, s, ga);
 }
 
 void launch_forward_gnn(hipStream_t s, const ForwardArgs& fa) {

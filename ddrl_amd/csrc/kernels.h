@@ -31,6 +31,7 @@ struct PolicyRoute {
 
 struct RouteArgs {
   int P, N, A, full_dim, n_agents, model;   // model: 0 ffn, 1 gnn
+  int e0;                                   // env range [e0, e0 + N) of a ranged observe (host env plane)
   PolicyRoute pol[DDRL_MAXP];
   float leg_angle[4];
 };
@@ -73,6 +74,7 @@ struct ActArgs {
   const float* eps;                // [N][n_agents][A]
   float* actions;                  // [N][8]
   int bootstrap;                   // 1: only value -> last_v
+  int e0, e1;                      // env range of this call ([0, N) for a whole step)
 };
 void launch_act_ffn(hipStream_t s, const RouteArgs& ra, const ActArgs& aa);
 void launch_act_gnn(hipStream_t s, const RouteArgs& ra, const ActArgs& aa);
@@ -92,6 +94,7 @@ struct RewardArgs {
   float* rec[DDRL_MAXP];
   RecLayout lay[DDRL_MAXP];
   int t;
+  int e0, n;                        // env range [e0, e0 + n) of this call (N: all envs)
 };
 void launch_reward(hipStream_t s, const RewardArgs& ra, const float* fw, const float* cfrc,
                    const float* actions, const uint8_t* done, uint8_t* done_tn);
@@ -132,8 +135,7 @@ struct UpdateHyper {
 // d / stride: the widest obs width / record stride of the launched policies
 void launch_update_ffn(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n, int A, int d,
                        int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp, int* err,
-                       unsigned* epoch_ctr,    // per-context launch counter (granule tags)
-                       int coherent);          // 1: device-coherent exchange stores (any placement)
+                       unsigned* epoch_ctr);   // per-context launch counter (granule tags)
 size_t gx_bytes(int P);
 // clip_by_global_norm + tf1 Adam on a flat (all-reduced) gradient vector
 // gscale multiplies the gradient before the clip (1 / ranks in the "local" data-parallel mode)
@@ -170,6 +172,7 @@ struct GnnArgs {
   float* normp;                  // [reduce blocks] squared-norm partials
   float* bp_cur;                 // [2] beta powers of the current step
   float* grad;                   // reduced gradient (scratch or the DDP output)
+  int act_e0, act_nfull;          // act: first env of the range, envs of the shard (record rows)
   // staged minibatch (fused update only): the records of this step, gathered by the previous
   // step's reduction ([128][stride]); rows = the row table [steps][128] of the schedule
   float* stage; const int32_t* rows; int stage_next;

@@ -58,7 +58,6 @@ struct UpdateBatch {
   int* err;              // set to 1 if an exchange timed out
   unsigned epoch;        // launch counter (12 bits, never 0): high bits of every exchange tag
   unsigned lds_bytes;    // dynamic LDS of the launch (bounds-checked build)
-  int coherent;          // 1: exchange stores are sc1 (any workgroup placement), see gx_put
 };
 
 // Bounds-checked diagnostic build (-DDDRL_BOUNDS, tools/build_diag.py): every staging,
@@ -374,9 +373,9 @@ __device__ __forceinline__ bool xchg_abandon(unsigned long long t0, int* err) {
 //  * default: plain stores into the XCD's shared L2 and sc1 polls (0.24 us per hop); correct
 //    when the workgroups that exchange share an L2, which every workgroup verifies at entry
 //    (its XCC id must be its policy's, block & 7: the dispatcher's round robin).  A misplaced
-//    workgroup raises error 2 and leaves; the launch option `coherent` (DDRL_XCHG_COHERENT=1)
-//    makes the stores sc1 (device-coherent write-through: the ISA of a relaxed agent-scope
-//    atomic store), valid for any placement, 0.50 us per hop.
+//    workgroup raises error 2 and leaves (the host then names the atomic build).  With coh
+//    set the stores are sc1 (device-coherent write-through: the ISA of a relaxed agent-scope
+//    atomic store), 0.50 us per hop.
 //  * -DDDRL_XCHG_ATOMIC: every granule access is a relaxed agent-scope 64-bit atomic
 //    (__hip_atomic_load / __hip_atomic_store): defined behaviour under the HIP memory model
 //    for any placement, each 8-byte {value, tag} half its own atomic.  The bounds-checked
@@ -507,9 +506,12 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   const int stride = U.lay.stride, cpr = stride >> 2, cpr_l = stg_chunks(stride, A);
 
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, q = lane >> 4, w = tid >> 6;
-  const bool coh = ub.coherent != 0;
+  // Store cache policy of the exchange.  A run-time choice here cost 0.3 us per step (the
+  // branches around every granule store, measured), so the device-coherent protocol is the
+  // separate -DDDRL_XCHG_ATOMIC build and this one always stores plainly into the XCD's L2.
+  constexpr bool coh = false;
 #ifndef DDRL_XCHG_ATOMIC
-  if (!coh) {   // the L2 protocol needs every workgroup of this policy on XCD p (see gx_put)
+  {   // the L2 protocol needs every workgroup of this policy on XCD p (see gx_put)
     unsigned xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     if ((xcc & 7u) != (unsigned)p) {
@@ -1035,9 +1037,8 @@ static void launch_update_t(hipStream_t s, UpdateBatch& ub, int P, int stride, i
 
 void launch_update_ffn(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n,
                        int A, int d, int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp,
-                       int* err, unsigned* epoch_ctr, int coherent) {
+                       int* err, unsigned* epoch_ctr) {
   UpdateBatch ub;
-  ub.coherent = coherent;
   for (int p = 0; p < DDRL_MAXP; ++p) ub.a[p] = p < h.P ? ua[p] : UpdateArgs{};
   ub.h = h;
   ub.nrows = nrows;

@@ -103,11 +103,12 @@ __global__ void k_observe_ffn(RouteArgs ra, const float* __restrict__ obs,
   filter_count(fc);
   const int p = blockIdx.y;
   const PolicyRoute& pr = ra.pol[p];
-  const int C = ra.N * pr.k;
+  const int C = ra.N * pr.k;              // rows of the env range [e0, e0 + N)
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= C * pr.d) return;
-  const int c = gid / pr.d, f = gid - c * pr.d;
-  const int e = c / pr.k, slot = c - e * pr.k;
+  const int cl = gid / pr.d, f = gid - cl * pr.d;
+  const int el = cl / pr.k, slot = cl - el * pr.k;
+  const int e = ra.e0 + el, c = ra.e0 * pr.k + cl;
   const int idx = pr.obs_index[slot][f];
   float v;
   if (idx < 0) {
@@ -213,10 +214,10 @@ __global__ void k_observe_gnn(RouteArgs ra, const float* __restrict__ obs,
   filter_count(fc);
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= ra.N * 4) return;
-  const int e = gid >> 2, n = gid & 3;
+  const int e = ra.e0 + (gid >> 2), n = gid & 3;
   const PolicyRoute& pr = ra.pol[0];
   const float* o = obs + (size_t)e * ra.full_dim;
-  float* x = X + (size_t)gid * 23;
+  float* x = X + ((size_t)e * 4 + n) * 23;
   for (int f = 0; f < 19; ++f) {
     const int idx = pr.obs_index[n][f];
     x[f] = norm_obs(o[idx], normc, idx, clip);
@@ -252,8 +253,9 @@ __global__ void __launch_bounds__(512) k_act_ffn(RouteArgs ra, ActArgs aa) {
   const int p = blockIdx.y;
   const PolicyRoute& pr = ra.pol[p];
   const int C = aa.C[p];
-  const int row0 = blockIdx.x * 64;
-  if (row0 >= C) return;
+  const int row_hi = aa.e1 * pr.k;        // rows of the env range [e0, e1)
+  const int row0 = aa.e0 * pr.k + blockIdx.x * 64;
+  if (row0 >= row_hi) return;
   const int d = pr.d;
   NetLds PW, VW;
   stage_weights(aa.theta[p], d, A, lds, PW, VW, 512);
@@ -263,7 +265,7 @@ __global__ void __launch_bounds__(512) k_act_ffn(RouteArgs ra, ActArgs aa) {
   const bool value_wave = w >= 4;
   if (aa.bootstrap && !value_wave) return;   // bootstrap: V(s_T) only
   const int row = row0 + 16 * (w & 3) + c;
-  const bool valid = row < C;
+  const bool valid = row < row_hi;
   const float* xs = aa.stage[p] + (size_t)(valid ? row : 0) * d;
   float xop[12];
 #pragma unroll
@@ -332,7 +334,7 @@ static void launch_act_t(hipStream_t s, dim3 grid, const RouteArgs& ra, const Ac
 
 void launch_act_ffn(hipStream_t s, const RouteArgs& ra, const ActArgs& aa) {
   int maxC = 0;
-  for (int p = 0; p < ra.P; ++p) maxC = max(maxC, aa.C[p]);
+  for (int p = 0; p < ra.P; ++p) maxC = max(maxC, (aa.e1 - aa.e0) * ra.pol[p].k);
   dim3 grid((maxC + 63) / 64, ra.P);
   int maxd = 0;
   for (int p = 0; p < ra.P; ++p) maxd = max(maxd, ra.pol[p].d);
@@ -348,8 +350,8 @@ __global__ void k_reward(RewardArgs ra, const float* __restrict__ fw, const floa
                          uint8_t* __restrict__ done_tn) {
   const int na = ra.n_agents;
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= ra.N * na) return;
-  const int e = gid / na, j = gid - e * na;
+  if (gid >= ra.n * na) return;
+  const int el = gid / na, j = gid - el * na, e = ra.e0 + el;
   const float* cf = cfrc + (size_t)e * 14 * 6;
   const float* a8 = actions + (size_t)e * 8;
   const double fwd = fw[e];
@@ -391,7 +393,7 @@ __global__ void k_reward(RewardArgs ra, const float* __restrict__ fw, const floa
 
 void launch_reward(hipStream_t s, const RewardArgs& ra, const float* fw, const float* cfrc,
                    const float* actions, const uint8_t* done, uint8_t* done_tn) {
-  const int n = ra.N * ra.n_agents;
+  const int n = ra.n * ra.n_agents;
   hipLaunchKernelGGL(k_reward, dim3((n + 255) / 256), dim3(256), 0, s, ra, fw, cfrc, actions,
                      done, done_tn);
 }

@@ -92,6 +92,18 @@ _SIGS = {
     "ddrl_last_values_get": ([VP, C.c_int, VP, C.c_size_t], C.c_int),
     "ddrl_last_values_set": ([VP, C.c_int, VP, C.c_size_t], C.c_int),
     "ddrl_done_set": ([VP, VP, C.c_size_t], C.c_int),
+    "ddrl_observe_range": ([VP, VP, C.c_int, C.c_int], C.c_int),
+    "ddrl_act_range": ([VP, C.c_int, C.c_int, C.c_int, VP, VP], C.c_int),
+    "ddrl_reward_range": ([VP, C.c_int, C.c_int, C.c_int, VP, VP, VP, VP], C.c_int),
+    "ddrl_hostenv_last_error": ([], C.c_char_p),
+    "ddrl_hostenv_create": ([C.c_int, C.c_int, C.c_int, C.c_uint64, f32, C.POINTER(VP)], C.c_int),
+    "ddrl_hostenv_destroy": ([VP], C.c_int),
+    "ddrl_hostenv_buffers": ([VP, C.POINTER(VP), C.POINTER(VP), C.POINTER(VP), C.POINTER(VP), C.POINTER(VP)],
+                             C.c_int),
+    "ddrl_hostenv_reset": ([VP], C.c_int),
+    "ddrl_hostenv_step": ([VP, C.c_int, C.c_int], C.c_int),
+    "ddrl_hostenv_threads": ([VP], C.c_int),
+    "ddrl_rollout_hostenv": ([VP, VP, C.c_int, VP, C.c_int], C.c_int),
 }
 
 _lib = None
@@ -367,6 +379,66 @@ class Context:
         _ck(self.lib.ddrl_ppo_update_ddp(self.h, pid, _ptr(shuffle_dev), perms.ctypes.data, E, nb,
                                          rows_per_rank, kl_coeff, grad_scale))
 
+    # ---- ranged rollout calls (env groups of a pipelined host env plane) ----
+    def observe_range(self, obs_dev, e0, e1):
+        _ck(self.lib.ddrl_observe_range(self.h, _ptr(obs_dev), e0, e1))
+
+    def act_range(self, t, e0, e1, eps_dev, actions_dev):
+        _ck(self.lib.ddrl_act_range(self.h, t, e0, e1, _ptr(eps_dev), _ptr(actions_dev)))
+
+    def reward_range(self, t, e0, e1, fw_dev, cfrc_dev, actions_dev, done_dev=None):
+        _ck(self.lib.ddrl_reward_range(self.h, t, e0, e1, _ptr(fw_dev), _ptr(cfrc_dev), _ptr(actions_dev),
+                                       _ptr(done_dev)))
+
+    def rollout_hostenv(self, env, eps_dev, groups=2, reset=False):
+        """A fragment with the envs stepped on the host (HostEnv), pipelined over env groups."""
+        _ck(self.lib.ddrl_rollout_hostenv(self.h, env.h, groups, _ptr(eps_dev), 1 if reset else 0))
+
     def policy_forward(self, pid, obs_dev, n, logits_dev, values_dev, node_dev=None):
         _ck(self.lib.ddrl_policy_forward(self.h, pid, _ptr(obs_dev), _ptr(node_dev), n,
                                          _ptr(logits_dev), _ptr(values_dev)))
+
+
+class HostEnv:
+    """The host env plane (hostenv.cpp): N QuAntruped stand-in envs stepped by a pool of host
+    threads into pinned buffers, exposed here as numpy views (obs [N][D], act [N][8], fw [N],
+    cfrc [N][14][6], done [N])."""
+
+    def __init__(self, n_envs, obs_dim=43, n_threads=1, seed=0, target_velocity=0.0):
+        self.lib = load()
+        h = VP()
+        if self.lib.ddrl_hostenv_create(n_envs, obs_dim, n_threads, seed, target_velocity, C.byref(h)) != 0:
+            raise DdrlError(self.lib.ddrl_hostenv_last_error().decode())
+        self.h, self.n, self.obs_dim = h, n_envs, obs_dim
+        ptrs = [VP() for _ in range(5)]
+        self._ck(self.lib.ddrl_hostenv_buffers(h, *[C.byref(p) for p in ptrs]))
+        view = lambda p, ct, shape: np.ctypeslib.as_array(C.cast(p, C.POINTER(ct)), shape=shape)
+        self.obs = view(ptrs[0], C.c_float, (n_envs, obs_dim))
+        self.act = view(ptrs[1], C.c_float, (n_envs, 8))
+        self.fw = view(ptrs[2], C.c_float, (n_envs,))
+        self.cfrc = view(ptrs[3], C.c_float, (n_envs, 14, 6))
+        self.done = view(ptrs[4], C.c_uint8, (n_envs,))
+        self.threads = self.lib.ddrl_hostenv_threads(h)
+
+    def _ck(self, rc):
+        if rc != 0:
+            raise DdrlError(self.lib.ddrl_hostenv_last_error().decode())
+
+    def reset(self):
+        self._ck(self.lib.ddrl_hostenv_reset(self.h))
+        return self.obs
+
+    def step(self, e0=0, e1=None):
+        """Step the envs [e0, e1) with the actions in self.act (written by the caller)."""
+        self._ck(self.lib.ddrl_hostenv_step(self.h, e0, self.n if e1 is None else e1))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.ddrl_hostenv_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

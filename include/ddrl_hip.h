@@ -136,6 +136,14 @@ int ddrl_act(ddrl_ctx* ctx, int t, const float* eps_dev, float* actions_dev);
 int ddrl_reward(ddrl_ctx* ctx, int t, const float* fw_dev, const float* cfrc_dev,
                 const float* actions_dev, const uint8_t* done_dev);
 int ddrl_bootstrap(ddrl_ctx* ctx);
+/* The same over the envs [e0, e1) only, on full-size buffers (obs_dev[N][D], eps_dev, actions_dev,
+ * fw_dev, cfrc_dev, done_dev): a pipelined host env plane (ddrl_rollout_hostenv) runs its env
+ * groups through these so that one group's host step overlaps another group's device work.
+ * The env-side filter pushes the range's rows as one batch (groups in call order). */
+int ddrl_observe_range(ddrl_ctx* ctx, const float* obs_dev, int e0, int e1);
+int ddrl_act_range(ddrl_ctx* ctx, int t, int e0, int e1, const float* eps_dev, float* actions_dev);
+int ddrl_reward_range(ddrl_ctx* ctx, int t, int e0, int e1, const float* fw_dev, const float* cfrc_dev,
+                      const float* actions_dev, const uint8_t* done_dev);
 /* A whole fragment over device-resident env data (a device env, replayed transitions, the
  * synthetic benchmark): for t in [0, T): act(t), reward(t), observe(obs_dev[t + 1]); then
  * bootstrap.  Expects observe(obs_dev[0]) to have been called.  Layouts: obs_dev[T+1][N][D],
@@ -158,6 +166,26 @@ int ddrl_step_host(ddrl_ctx* ctx, int t, const float* obs_host, const float* eps
 int ddrl_act_host(ddrl_ctx* ctx, int t, const float* eps_host, float* actions_host);
 int ddrl_env_step_host(ddrl_ctx* ctx, int t, const float* fw_host, const float* cfrc_host,
                        const uint8_t* done_host, const float* obs_next_host);
+
+/* f1 host env plane (hostenv.cpp): a vectorized QuAntruped stand-in (clean-room kinematics in
+ * the reference env's layout -- MuJoCo is absent; see hostenv.h) stepped by a pool of
+ * n_threads host threads into pinned buffers obs[N][obs_dim], act[N][8], fw[N],
+ * cfrc[N][14][6], done[N] (ddrl_hostenv_buffers).  Replaces the reference's per-worker
+ * MuJoCo stepping (simulation_envs/quantruped_v3.py:166-267) and the adaptor's
+ * step(action_dict) (quantruped_adaptor_multi_environment.py:220-250).
+ *   step: the envs [e0, e1) with act[e][8] (clipped to [-1, 1]); a done env is reset at once.
+ * ddrl_rollout_hostenv runs a whole fragment over it, pipelined over `groups` env groups (one
+ * group's host step overlaps the other groups' device work and transfers), then bootstraps. */
+typedef struct ddrl_hostenv ddrl_hostenv;
+const char* ddrl_hostenv_last_error(void);
+int ddrl_hostenv_create(int n_envs, int obs_dim, int n_threads, uint64_t seed, float target_velocity,
+                        ddrl_hostenv** out);
+int ddrl_hostenv_destroy(ddrl_hostenv* env);
+int ddrl_hostenv_buffers(ddrl_hostenv* env, float** obs, float** act, float** fw, float** cfrc, uint8_t** done);
+int ddrl_hostenv_reset(ddrl_hostenv* env);
+int ddrl_hostenv_step(ddrl_hostenv* env, int e0, int e1);
+int ddrl_hostenv_threads(ddrl_hostenv* env);
+int ddrl_rollout_hostenv(ddrl_ctx* ctx, ddrl_hostenv* env, int groups, const float* eps_dev, int reset);
 
 /* Postprocessing: GAE over the fragment for every policy + advantage standardization
  * statistics (a11/a12). */

@@ -150,3 +150,93 @@ def test_rank_seeds_differ_per_rank_and_keep_rank0():
     assert seeds[0] == (3, 4)                     # single-process seeds unchanged
     flat = [s for pair in seeds for s in pair]
     assert len(set(flat)) == len(flat)            # no two ranks (or streams) share a seed
+
+
+# f1: the host env plane's stand-in envs (hostenv.cpp) -- deterministic, thread-count
+# invariant, the reference env's observation layout (no GPU needed: unpinned buffers here)
+def test_host_env_plane_is_deterministic_and_thread_invariant():
+    runs = []
+    for threads in (1, 3):
+        e = N.HostEnv(37, 44, threads, seed=5, target_velocity=0.5)
+        e.reset()
+        rng = np.random.default_rng(2)
+        out = []
+        for _ in range(60):
+            e.act[:] = rng.uniform(-1.5, 1.5, size=(37, 8)).astype(np.float32)
+            e.step(0, 20)
+            e.step(20, 37)
+            out.append((e.obs.copy(), e.fw.copy(), e.cfrc.copy(), e.done.copy()))
+        runs.append(out)
+        assert e.threads == threads
+        e.close()
+    for a, b in zip(*runs):
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+    obs = np.stack([o[0] for o in runs[0]])
+    assert np.isfinite(obs).all()
+    assert np.all(obs[:, :, 43] == np.float32(0.5))            # TVel column
+    # ctrl columns 35..42 are the clipped actions of the step (0 right after a reset)
+    assert np.abs(obs[:, :, 35:43]).max() <= 1.0
+    quat = obs[:, :, 1:5].astype(np.float64)
+    np.testing.assert_allclose(np.linalg.norm(quat, axis=-1), 1.0, atol=1e-6)
+    cf = np.stack([o[2] for o in runs[0]])
+    assert (cf[:, :, 0] == 0).all() and cf[:, :, 4::3, 5].max() > 0      # floor body: no force; feet touch
+
+
+def test_host_env_rejects_bad_arguments():
+    with pytest.raises(N.DdrlError):
+        N.HostEnv(0, 43)
+    with pytest.raises(N.DdrlError):
+        N.HostEnv(8, 40)
+    e = N.HostEnv(8, 43)
+    with pytest.raises(N.DdrlError):
+        e.step(4, 4)
+    e.close()
+
+
+@pytest.mark.parametrize("env_name,config", [
+    ("QuantrupedMultiEnv_Local", {}),
+    ("QuantrupedMultiEnv_FullyDecentralGlobalCost", {}),
+    ("QuantrupedMultiEnv_TwoSides", {"norm_reward": True}),
+    ("QuantrupedMultiEnv_SharedDecentralLegTransforms", {}),
+    ("QuantrupedMultiEnv_Centralized", {"target_velocity": [0.5]}),
+])
+def test_dict_api_over_host_env_plane_matches_oracle(env_name, config):
+    """MultiAgentEnv reset() / step(action_dict) over the host env plane (ddrl_amd.hostenv):
+    filter, distribute_observations, concatenate_actions and the rewards against the oracle
+    on the env plane's own raw outputs (adaptor :83-85, :124-136, :160-212, :214-250)."""
+    from oracle import ddrl_oracle as O
+    from ddrl_amd.hostenv import HostMultiAgentEnv
+    env = HostMultiAgentEnv(env_name, config, n_envs=1, seed=4)
+    spec = env.spec
+    rs = O.RunningStat((env.D,))
+    obs = env.reset()
+    ref = O.distribute_observations(O.mean_std_filter(env.env.obs[0], rs, True, 10.0), spec.obs_indices)
+    assert set(obs) == set(spec.agent_names)
+    for a in obs:
+        np.testing.assert_allclose(obs[a], ref[a], rtol=1e-12, atol=1e-12)
+    rng = np.random.default_rng(0)
+    tables = {a: spec.contact_force_indices[a] for a in spec.agent_names}
+    for _ in range(30):
+        actions = {a: rng.uniform(-1.2, 1.2, size=len(spec.action_indices[a])) for a in spec.agent_names}
+        obs, rew, done, info = env.step(actions)
+        applied = env.env.act[0].astype(np.float64)
+        sign = {a: np.where(np.asarray(getattr(spec, "action_negate", {}).get(a, [False] * 8))[:len(spec.action_indices[a])], -1.0, 1.0)
+                for a in spec.agent_names}
+        want = O.concatenate_actions({a: np.clip(v, -1, 1) * sign[a] for a, v in actions.items()}, spec.action_indices)
+        np.testing.assert_allclose(applied, want.astype(np.float32))
+        per_agent = {a: applied[spec.action_indices[a]] for a in spec.agent_names}
+        fw, cfrc = float(env.env.fw[0]), env.env.cfrc[0].astype(np.float64)
+        if spec.reward_mode == "global":
+            rref = O.global_reward(fw, cfrc, per_agent, spec.ctrl_cost_weight, spec.contact_cost_weight)
+        else:
+            rref = O.per_leg_reward(fw, cfrc, per_agent, tables, spec.ctrl_cost_weight, spec.contact_cost_weight,
+                                    norm_reward=spec.reward_mode == "norm")
+        for a in spec.agent_names:
+            assert rew[a] == pytest.approx(rref[a], rel=1e-12, abs=1e-12)
+        oref = O.distribute_observations(O.mean_std_filter(env.env.obs[0], rs, True, 10.0), spec.obs_indices)
+        for a in obs:
+            np.testing.assert_allclose(obs[a], oref[a], rtol=1e-12, atol=1e-12)
+        assert set(done) == {"__all__"} and isinstance(done["__all__"], bool)
+        assert info["reward_forward"] == fw
+    env.close()
