@@ -270,11 +270,10 @@ static int check_err(ddrl_ctx* c) {
   HIPCHK(hipMemcpy(&e, c->err, sizeof(int), hipMemcpyDeviceToHost));
   if (e) {
     (void)hipMemset(c->err, 0, sizeof(int));
-    if (e == 2)
-      return fail("update kernel: a workgroup was not placed on its policy's XCD, so the XCD-local exchange "
-                  "protocol cannot run (build the atomic-exchange library, `python -m ddrl_amd.build --atomic`, "
-                  "and run with DDRL_LIB=libddrl_hip_atomic.so)");
-    return fail("update kernel: norm exchange between the policy and value workgroups timed out");
+    return fail("update kernel: an exchange between the workgroups of a policy timed out (3 s).  The "
+                "default protocol needs the workgroups of one policy on one XCD (round-robin dispatch); if "
+                "this machine places them otherwise, build the atomic-exchange library (`python -m "
+                "ddrl_amd.build --atomic`) and run with DDRL_LIB=libddrl_hip_atomic.so");
   }
   return 0;
 }

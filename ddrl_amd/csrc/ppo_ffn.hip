@@ -371,11 +371,13 @@ __device__ __forceinline__ bool xchg_abandon(unsigned long long t0, int* err) {
 }
 // Two builds of the same protocol:
 //  * default: plain stores into the XCD's shared L2 and sc1 polls (0.24 us per hop); correct
-//    when the workgroups that exchange share an L2, which every workgroup verifies at entry
-//    (its XCC id must be its policy's, block & 7: the dispatcher's round robin).  A misplaced
-//    workgroup raises error 2 and leaves (the host then names the atomic build).  With coh
-//    set the stores are sc1 (device-coherent write-through: the ISA of a relaxed agent-scope
-//    atomic store), 0.50 us per hop.
+//    when the workgroups that exchange share an L2.  The dispatcher deals a grid's blocks to
+//    the 8 XCDs round robin, from a start XCD that varies between dispatches (measured: a
+//    data-parallel gradient launch found block p on XCD != p), so blocks b = p mod 8 -- the
+//    workgroups of policy p -- always share one XCD.  Were that ever broken, a poll would
+//    never see its partner: the 3 s bound raises the error word and the host names the
+//    atomic build.  With coh set the stores are sc1 (device-coherent write-through: the ISA
+//    of a relaxed agent-scope atomic store), 0.50 us per hop.
 //  * -DDDRL_XCHG_ATOMIC: every granule access is a relaxed agent-scope 64-bit atomic
 //    (__hip_atomic_load / __hip_atomic_store): defined behaviour under the HIP memory model
 //    for any placement, each 8-byte {value, tag} half its own atomic.  The bounds-checked
@@ -510,16 +512,6 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   // branches around every granule store, measured), so the device-coherent protocol is the
   // separate -DDDRL_XCHG_ATOMIC build and this one always stores plainly into the XCD's L2.
   constexpr bool coh = false;
-#ifndef DDRL_XCHG_ATOMIC
-  {   // the L2 protocol needs every workgroup of this policy on XCD p (see gx_put)
-    unsigned xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    if ((xcc & 7u) != (unsigned)p) {
-      if (tid == 0) atomicExch(ub.err, 2);   // the partners see it at their first slow wait
-      return;
-    }
-  }
-#endif
   int row_l[RT];
   bool row_ok[RT];
 #pragma unroll
