@@ -279,12 +279,17 @@ class PPOTrainer:
         file is executed).  Returns the policy ids loaded."""
         from .rllib_checkpoint import policy_ids, policy_state, read_checkpoint
         ck = read_checkpoint(path)
-        have = policy_ids(ck)
-        missing = [pid for pid in self.policy_ids if pid not in have]
+        return self.load_policy_states({pid: policy_state(ck, pid) for pid in policy_ids(ck)})
+
+    def load_policy_states(self, states):
+        """Per policy id: {"weights", "adam_m", "adam_v", "beta_powers", "filter" (n, M, S) or
+        None, "kl_coeff" or None} (ddrl_amd.rllib_checkpoint.policy_state's layout) into the
+        context; returns the policy ids loaded."""
+        missing = [pid for pid in self.policy_ids if pid not in states]
         if missing:
-            raise ValueError(f"checkpoint has policies {have}, this env needs {self.policy_ids}")
+            raise ValueError(f"checkpoint has policies {sorted(states)}, this env needs {self.policy_ids}")
         for p, pid in enumerate(self.policy_ids):
-            st = policy_state(ck, pid)
+            st = states[pid]
             if st["weights"].size != self.ctx.n_params[p]:
                 raise ValueError(f"{pid}: checkpoint holds {st['weights'].size} parameters, the model "
                                  f"{self.ctx.n_params[p]}")

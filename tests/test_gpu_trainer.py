@@ -118,3 +118,75 @@ def test_ddp_learner_hip_backend_matches_oracle(pg1):
     kl_ref = np.mean([s["kl"] for s in stats[-pe.shape[1]:]])
     np.testing.assert_allclose(kl, kl_ref, rtol=1e-4)
     ctx.close()
+
+
+def _ddp_rank(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)          # both ranks share the one GPU of the box
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ddrl_amd.trainer import PPOTrainer
+    tr = PPOTrainer({"env": "QuantrupedMultiEnv_SharedDecentral", "rollout_fragment_length": 8,
+                     "parallel": "ddp", "observation_filter": "MeanStdFilter"}, n_envs=32, seed=5)
+    w0 = tr.get_weights()["policy_legs"] if "policy_legs" in tr.policy_ids else next(iter(tr.get_weights().values()))
+    r = tr.train()
+    pid = tr.policy_ids[0]
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), rec=tr.ctx.records_get(0), w0=w0, w1=tr.get_weights()[pid],
+             env_filter_n=np.array([tr.ctx.filter_get()[0]]), env_filter_M=tr.ctx.filter_get()[1],
+             pf_M=tr.ctx.policy_filter_get(0)[1], kl=np.array([r["info"]["learner"][pid]["kl"]]))
+    tr.stop()
+    dist.destroy_process_group()
+
+
+def test_trainer_ddp_world2_ranks_sample_differently_and_agree_on_weights():
+    """two data-parallel ranks (gloo, sharing the box's GPU) sample DIFFERENT
+    trajectories (env and exploration seeds offset by rank) and hold IDENTICAL weights after an
+    update (gradient all-reduce, identical Adam); RLlib's per-policy filter is synchronized,
+    the env-side filter stays rank-local (a per-process singleton in the reference)."""
+    import tempfile
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = tempfile.mkdtemp()
+    mp.spawn(_ddp_rank, args=(2, port, out), nprocs=2, join=True)
+    a, b = (np.load(os.path.join(out, f"r{r}.npz")) for r in range(2))
+    np.testing.assert_array_equal(a["w0"], b["w0"])              # same init
+    assert not np.array_equal(a["rec"], b["rec"])                # different trajectories
+    assert not np.array_equal(a["w1"], a["w0"])                  # the update moved the weights
+    np.testing.assert_array_equal(a["w1"], b["w1"])              # ... identically on both ranks
+    np.testing.assert_array_equal(a["pf_M"], b["pf_M"])          # per-policy filter synced
+    assert a["env_filter_n"][0] == b["env_filter_n"][0] == 32 * 9   # env filter: own pushes only
+    assert not np.array_equal(a["env_filter_M"], b["env_filter_M"])
+    assert a["kl"][0] == b["kl"][0]                              # all-reduced KL
+
+
+def test_trainer_continues_from_published_local_checkpoint():
+    """PPOTrainer.load_policy_states (the back end of restore_rllib) with the published Local
+    policies (tests/golden/ckpt_local_1250.npz): weights, Adam state, filters and KL
+    coefficients land in the context, and a training iteration continues from them."""
+    import json
+    from ddrl_amd.trainer import PPOTrainer
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ckpt_local_1250.npz"),
+                allow_pickle=False)
+    pids = json.loads(bytes(z["policy_ids"]).decode())
+    states = {pid: {"weights": z[f"{pid}/weights"], "adam_m": z[f"{pid}/adam_m"], "adam_v": z[f"{pid}/adam_v"],
+                    "beta_powers": tuple(float(x) for x in z[f"{pid}/beta_powers"]),
+                    "filter": (float(z[f"{pid}/filter_n"][0]), z[f"{pid}/filter_M"], z[f"{pid}/filter_S"]),
+                    "kl_coeff": float(z[f"{pid}/kl_coeff"][0])} for pid in pids}
+    tr = PPOTrainer({"env": "QuantrupedMultiEnv_Local", "rollout_fragment_length": 8,
+                     "observation_filter": "MeanStdFilter"}, n_envs=32, seed=2)
+    assert tr.load_policy_states(states) == tr.policy_ids
+    for p, pid in enumerate(tr.policy_ids):
+        np.testing.assert_array_equal(tr.ctx.params_get(p), states[pid]["weights"])
+        m, v, b1, b2 = tr.ctx.adam_get(p)
+        np.testing.assert_array_equal(v, states[pid]["adam_v"])
+        assert tr.kl_coeff[p] == states[pid]["kl_coeff"]
+        assert tr.ctx.policy_filter_get(p)[0] == states[pid]["filter"][0]
+    r = tr.train()
+    for pid, st in r["info"]["learner"].items():
+        assert np.isfinite(st["total_loss"]) and st["cur_kl_coeff"] == pytest.approx(states[pid]["kl_coeff"], rel=1e-6)
+    tr.stop()
