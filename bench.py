@@ -361,7 +361,8 @@ def main():
         active_cus = 2 * ((rows_per_step + 3) // 4)
         model = f"shared GraphNet/MPNN leg policy (4 nodes x 19 features + ego quaternion, A={A})"
     else:
-        kernel = (f"k_update_ffn<{A}, {ks1}> grad + RCCL all-reduce + k_apply_adam per step" if ddp else
+        coll = "RCCL" if backend == "nccl" else backend
+        kernel = (f"k_update_ffn<{A}, {ks1}> grad + {coll} all-reduce + k_apply_adam per step" if ddp else
                   "k_update_ffn (fused PPO minibatch SGD, one launch per iteration)")
         # the fused launch keeps 2 workgroups (policy / value branch) per policy, one per CU,
         # times the row split (DDRL_UPDATE_SPLIT, default 2; the data-parallel grad launch is unsplit)
