@@ -29,27 +29,22 @@ Pool::~Pool() {
 }
 
 void Pool::run(int) {
+  // A worker takes chunks only of the generation it woke up for: a worker still looping after
+  // the last chunk of generation g was finished must not pick up a chunk of g + 1 with g's job
+  // (the caller's function object is gone by then).
   uint64_t seen = 0;
+  std::unique_lock<std::mutex> lk(mu_);
   for (;;) {
-    const std::function<void(int, int)>* job;
-    {
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait(lk, [&] { return stop_ || generation_ != seen; });
-      if (stop_) return;
-      seen = generation_;
-      job = job_;
-    }
-    for (;;) {
-      int c;
-      {
-        std::lock_guard<std::mutex> lk(mu_);
-        if (next_ >= chunks_) break;
-        c = next_++;
-      }
-      const int lo = (int)((long long)n_ * c / chunks_), hi = (int)((long long)n_ * (c + 1) / chunks_);
-      (*job)(lo, hi);
-      std::lock_guard<std::mutex> lk(mu_);
-      if (++finished_ == chunks_) done_cv_.notify_all();
+    cv_.wait(lk, [&] { return stop_ || generation_ != seen; });
+    if (stop_) return;
+    seen = generation_;
+    const std::function<void(int, int)>* job = job_;
+    while (generation_ == seen && next_ < chunks_) {
+      const int c = next_++, n = n_, ch = chunks_;
+      lk.unlock();
+      (*job)((int)((long long)n * c / ch), (int)((long long)n * (c + 1) / ch));
+      lk.lock();
+      if (++finished_ == ch) done_cv_.notify_all();
     }
   }
 }
@@ -190,7 +185,16 @@ void ddrl_hostenv::step_env(int e, const float* a8) {
     s.pitch += kH * s.wpitch;
   }
   ++s.steps;
-  fw[e] = (float)((s.x - x0) / kDt);
+  // forward reward of the step (quantruped_v3.py:163-179): the torso's x velocity; the TVel
+  // envs reward reaching the target velocity instead (QuAntrupedTVelEnv.compute_forward_reward,
+  // quantruped_v3.py:391-392)
+  const double vx = (s.x - x0) / kDt;
+  if (D > 43) {
+    const double tv = target_velocity;
+    fw[e] = (float)((1.0 + 1.0 / tv) * (1.0 / (std::fabs(vx - tv) + 1.0) - 1.0 / (tv + 1.0)));
+  } else {
+    fw[e] = (float)vx;
+  }
   // cfrc_ext [14][6]: {floor, torso, then hip / leg / foot of FL, HL, HR, FR}; rotational then
   // linear part, the contact force on the foot bodies
   float* cf = cfrc + (size_t)e * 14 * 6;
@@ -241,8 +245,9 @@ extern "C" const char* ddrl_hostenv_last_error(void) { return g_henv_err.c_str()
 
 extern "C" int ddrl_hostenv_create(int n_envs, int obs_dim, int n_threads, uint64_t seed, float target_velocity,
                                    ddrl_hostenv** out) {
-  if (!out || n_envs < 1 || (obs_dim != 43 && obs_dim != 44) || n_threads < 1) {
-    g_henv_err = "ddrl_hostenv_create: n_envs >= 1, obs_dim 43 or 44, n_threads >= 1";
+  if (!out || n_envs < 1 || (obs_dim != 43 && obs_dim != 44) || n_threads < 1 ||
+      (obs_dim == 44 && !(target_velocity > 0.f))) {
+    g_henv_err = "ddrl_hostenv_create: n_envs >= 1, obs_dim 43 or 44 (44: target_velocity > 0), n_threads >= 1";
     return -1;
   }
   auto* h = new ddrl_hostenv();

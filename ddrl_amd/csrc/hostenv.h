@@ -10,7 +10,8 @@
 // frame_skip 5 at dt 0.01 (0.05 s per env step, quantruped_v3.py's dt).  It emits exactly what
 // the device path consumes: obs43 = [qpos[2:15] (z, quaternion w x y z, 8 joint angles),
 // qvel (14), actuator + constraint forces (8), ctrl (8)] (+ target velocity as column 44 for the
-// TVel envs), the forward reward fw = dx / dt, cfrc_ext [14 bodies][6] (contact force on each
+// TVel envs), the forward reward fw = dx / dt (TVel: the target-velocity reward of
+// quantruped_v3.py:391-392), cfrc_ext [14 bodies][6] (contact force on each
 // foot body) and done (gym TimeLimit at 1000 steps, or torso height out of [0.1, 1.5]); a done
 // env is reset at once (its next observation is the reset one), as RLlib's sampler does.
 // Every env is a pure function of (seed, env index, its own actions): results do not depend on

@@ -159,6 +159,12 @@ def per_leg_reward(fw_reward, cfrc_ext, action_dict, contact_tables, ctrl_w, con
     return rew
 
 
+def tvel_forward_reward(x_velocity, target_velocity):
+    """QuAntrupedTVelEnv.compute_forward_reward (simulation_envs/quantruped_v3.py:391-392)."""
+    tv = float(target_velocity)
+    return (1.0 + 1.0 / tv) * (1.0 / (np.abs(x_velocity - tv) + 1.0) - 1.0 / (tv + 1.0))
+
+
 def global_reward(fw_reward, cfrc_ext, action_dict, ctrl_w, contact_w):
     """:173-186"""
     contact = contact_w * np.sum(np.square(np.clip(cfrc_ext, -1.0, 1.0)))

@@ -183,9 +183,33 @@ def test_host_env_plane_is_deterministic_and_thread_invariant():
     assert (cf[:, :, 0] == 0).all() and cf[:, :, 4::3, 5].max() > 0      # floor body: no force; feet touch
 
 
+def test_host_env_tvel_forward_reward_matches_oracle():
+    """f4: the TVel envs' forward reward (quantruped_v3.py:391-392) -- the same dynamics as the
+    plain env (the target velocity is only observed), fw = the target-velocity reward of the
+    torso's x velocity; 1.0 at the target, the reward of the plain env elsewhere."""
+    from oracle import ddrl_oracle as O
+    envs = [N.HostEnv(16, 43, 2, seed=9), N.HostEnv(16, 44, 2, seed=9, target_velocity=0.75)]
+    for e in envs:
+        e.reset()
+    rng = np.random.default_rng(4)
+    for _ in range(40):
+        a = rng.uniform(-1, 1, size=(16, 8)).astype(np.float32)
+        for e in envs:
+            e.act[:] = a
+            e.step()
+        np.testing.assert_array_equal(envs[0].obs, envs[1].obs[:, :43])
+        np.testing.assert_allclose(envs[1].fw, O.tvel_forward_reward(envs[0].fw.astype(np.float64), 0.75),
+                                   rtol=1e-5, atol=1e-6)
+    assert O.tvel_forward_reward(0.75, 0.75) == pytest.approx(1.0)
+    for e in envs:
+        e.close()
+
+
 def test_host_env_rejects_bad_arguments():
     with pytest.raises(N.DdrlError):
-        N.HostEnv(0, 43)
+        N.HostEnv(44 - 44, 43)
+    with pytest.raises(N.DdrlError):
+        N.HostEnv(8, 44)            # TVel needs a target velocity
     with pytest.raises(N.DdrlError):
         N.HostEnv(8, 40)
     e = N.HostEnv(8, 43)
@@ -240,3 +264,22 @@ def test_dict_api_over_host_env_plane_matches_oracle(env_name, config):
         assert set(done) == {"__all__"} and isinstance(done["__all__"], bool)
         assert info["reward_forward"] == fw
     env.close()
+
+
+def test_host_env_thread_pool_many_small_jobs():
+    """The pool under back-to-back small jobs (more threads than chunks, 3,000 jobs): a worker
+    that finishes late must never run a chunk of the next job with the previous job's function
+    (the generation check in hostenv::Pool::run); results equal the single-threaded env."""
+    runs = []
+    for threads in (8, 1):
+        e = N.HostEnv(5, 43, threads, seed=3)
+        e.reset()
+        rng = np.random.default_rng(1)
+        for _ in range(1500):
+            e.act[:] = rng.uniform(-1, 1, size=(5, 8)).astype(np.float32)
+            e.step(0, 2)
+            e.step(2, 5)
+        runs.append((e.obs.copy(), e.fw.copy()))
+        e.close()
+    np.testing.assert_array_equal(runs[0][0], runs[1][0])
+    np.testing.assert_array_equal(runs[0][1], runs[1][1])
