@@ -37,6 +37,32 @@
 #define GNI 5              // feature rows i per wave (ceil(19 / 4))
 
 enum { GNN_ACT = 0, GNN_FWD = 1, GNN_GRAD = 2 };
+// Gradient launches split each tile's backward over GNN_Z workgroups (blockIdx.z): all of
+// them run the forward (the backward needs every activation), workgroup z then computes only
+// the hypernetwork feature rows k % GNN_Z == z of each wave and its Wnode / Wmsg tile slots
+// (gnn_tile_owner); every partial is still written by exactly one workgroup.  Measured at C5
+// (2048 envs): Z = 1 / 2 / 4 / 5 -> 25.2 / 24.4 / 21.9 / 24.9 us per step (Z = 5 puts two
+// workgroups on some CUs: 320 > 256).
+#ifndef DDRL_GNN_Z
+#define DDRL_GNN_Z 4
+#endif
+constexpr int GNN_Z = DDRL_GNN_Z;
+static_assert(GNN_Z >= 1 && GNN_Z <= GNI, "split of the gradient backward");
+// Owner of the Wnode / Wmsg tile slot k (0..7) of each wave.  With four shares, share 0's
+// waves 0-2 also carry the hypernetwork rows 16-18 (19 rows over 16 waves), so its tile
+// slots go to shares 1-3 (measured 0.26 us per step shorter at C5 than k % 4).
+__device__ __forceinline__ int gnn_tile_owner(int k) {
+#ifdef DDRL_GNN_TILE_MOD
+  return k % GNN_Z;
+#endif
+  return GNN_Z == 4 ? 1 + k % 3 : k % GNN_Z;
+}
+// Owner of the hypernetwork backward's (feature row slot k, 16-column block t) of each wave:
+// row slot k % GNN_Z, except that with four shares the last slot (rows 16-18, waves 0-2) is
+// dealt by column block, so no wave carries two whole rows.
+__device__ __forceinline__ int gnn_hbwd_owner(int k, int t) {
+  return (GNN_Z == 4 && k == GNI - 1) ? t : k % GNN_Z;
+}
 
 struct GnnNetOff { int wenc, benc, wmsg, wnode, wout, bout; };
 __host__ __device__ inline GnnNetOff gnn_net_off(int A, int net) {
@@ -306,7 +332,8 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
   }
   __syncthreads();
   // per-tile statistics partial (fixed order over the 4 graphs)
-  if (tid < 5) {
+  const int zs = (int)blockIdx.z;   // backward share of this workgroup (0 .. GNN_Z - 1)
+  if (tid < 5 && zs == 0) {
     float s = 0.f;
     for (int gg = 0; gg < 4; ++gg) s += (4 * tile + gg < ga.n_graphs) ? sts[gg * 8 + tid] : 0.f;
     ga.statp[(NET * (DDRL_MB / 4) + tile) * 8 + tid] = s;
@@ -317,7 +344,8 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
 #pragma unroll
   for (int o = 0; o < O; ++o) ds[o] = is_sel ? dsh[g * 4 + o] : 0.f;
   // dWout / dbout
-  if constexpr (O == 4) {
+  if (zs != 0) {
+  } else if constexpr (O == 4) {
     float v[16];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
@@ -332,7 +360,7 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
       if (c == 0) P[off.wout + (16 * w + 4 * q + r) * O] = v;
     }
   }
-  if (tid < O) {
+  if (tid < O && zs == 0) {
     float s = 0.f;
     for (int gg = 0; gg < 4; ++gg) s += dsh[gg * 4 + tid] * (4 * tile + gg < ga.n_graphs ? 1.f : 0.f);
     P[off.bout + tid] = s;
@@ -377,9 +405,10 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
   // the hypernet partials are consumed: reuse PART for the dz exchange [block][r][lane]
 #pragma unroll
   for (int r = 0; r < 4; ++r) part[(4 * w + r) * 64 + lane] = dh[r] * (1.f - h[w][r] * h[w][r]);
-  // dWnode, dWmsg: 32 tiles of 16x16 over the 16 rows, 8 per wave
+  // dWnode, dWmsg: 32 tiles of 16x16 over the 16 rows, 8 per wave (k % GNN_Z == zs here)
 #pragma unroll 2
   for (int k = 0; k < 8; ++k) {
+    if (gnn_tile_owner(k) != zs) continue;
     const int id = w + 4 * k;            // 0..31
     const int mat = id >> 4, kb = (id >> 2) & 3, ob = id & 3;
     const floatx4 t = dw_tile<16>(himg, mat ? dmimg : duimg, kb, ob);
@@ -428,6 +457,40 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
   };
   constexpr int NK = (GF + 3) / 4;   // feature rows of wave 0 (waves 1..3 have NK or NK - 1)
   static_assert(NK == GNI, "feature rows per wave");
+  if constexpr (GNN_Z > 1) {
+    // this workgroup's (row k, column block t) pairs (gnn_hbwd_owner), not pipelined
+#pragma unroll
+    for (int k = 0; k < GNI; ++k) {
+      const int i = w + 4 * k;
+      bool any = false;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) any = any || gnn_hbwd_owner(k, t) == zs;
+      if (!any || i >= GF) continue;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (gnn_hbwd_owner(k, t) != zs) continue;
+        const floatx4 pre = mfma4(we[k][t], qv, be[k][t]);
+        floatx4 dp;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float wn = tanh_fast(pre[r]);
+          dp[r] = fi[k] * dz[t][r] * (1.f - wn * wn);
+        }
+        *reinterpret_cast<floatx4*>(tpb + 256 * t + c * 16 + 4 * q) = dp;
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (gnn_hbwd_owner(k, t) != zs) continue;
+        floatx4 acc = splat4(0.f);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) acc = mfma4(tpb[256 * t + (4 * s4 + q) * 16 + c], qb[s4], acc);
+        const int j = i * 64 + 16 * t + 4 * q;
+        if (c < 4) *reinterpret_cast<floatx4*>(P + off.wenc + c * GHE + j) = acc;
+        else if (c == 4) *reinterpret_cast<floatx4*>(P + off.benc + j) = acc;
+      }
+    }
+    return;
+  }
   dpre_tiles(0, tpb);
 #pragma unroll
   for (int k = 0; k < GNI; ++k) {
@@ -488,7 +551,11 @@ __global__ void __launch_bounds__(256) k_gnn_reduce(GnnArgs ga, int ntiles, int 
   // issued after the partial loads, so its dependent row-table -> record chain waits behind
   // them instead of holding them back
   int sdst = -1;
+#ifdef DDRL_ABL_GNN_NO_STAGE_NEXT   // ablation build (timing only)
+  const float sv_next = 0.f;
+#else
   const float sv_next = ga.stage_next ? gnn_stage_load(ga, ga.step + 1, p, sdst) : 0.f;
+#endif
   float s = 0.f;
 #pragma unroll
   for (int t = 0; t < DDRL_MB / 4; ++t) s += v[t];
@@ -639,7 +706,7 @@ void launch_step_gnn(hipStream_t s, const UpdateArgs& u, const UpdateHyper& h, i
   const int ntiles = (nrows + 3) / 4;
   const int n = gnn_param_total(u.A);
   // tiles of the critic write their statistics after the actor's: statp [2][32][8]
-  hipLaunchKernelGGL((k_gnn<2, GNN_GRAD>), dim3(ntiles, 2), dim3(256), 0, s, ga);
+  hipLaunchKernelGGL((k_gnn<2, GNN_GRAD>), dim3(ntiles, 2, GNN_Z), dim3(256), 0, s, ga);
   const int nred = (n + 255) / 256;
 #ifdef DDRL_ABL_GNN_GRAD_ONLY   // ablation build (timing only): no reduction / Adam launches
   return;
