@@ -230,10 +230,7 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
     c->gnn.grad = c->pol[0].grad;
     rc = dalloc(c, &c->gnn.part, (size_t)(DDRL_MB / 4) * c->gnn.part_stride) || dalloc(c, &c->gnn.statp, 2 * (DDRL_MB / 4) * 8) ||
          dalloc(c, &c->gnn.normp, (np + 255) / 256) || dalloc(c, &c->gnn.bp_cur, 2) ||
-         dalloc(c, &c->gnn.stage, (size_t)DDRL_MB * c->pol[0].lay.stride);
-    // the fused update's row table: one entry per (minibatch step, row) of the schedule
-    c->gnn.rows_cap = (size_t)g.num_sgd_iter * c->pol[0].nb * DDRL_MB;
-    rc = rc || dalloc(c, &c->gnn.rows, c->gnn.rows_cap);
+         dalloc(c, &c->gnn.chunk, (size_t)GNN_CHUNK_STEPS * DDRL_MB * c->pol[0].lay.stride);
   }
   if (!rc) {
     float* tab[DDRL_MAXP] = {nullptr};
@@ -731,10 +728,16 @@ int ddrl_ppo_update(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const 
                       c->cfg.leg_coupling, c->xchg, c->gx, c->update_split, c->err, &c->upd_epoch);
   else if (c->pol[0].last_steps > 0) {   // one shared policy
     const int last = c->pol[0].last_steps;
-    launch_gnn_schedule(c->stream, ua[0], last, 0, c->gnn);
-    for (int step = 0; step < last; ++step)
-      launch_step_gnn(c->stream, ua[0], h, step, 128, 1.f / c->cfg.sgd_minibatch_size, c->gnn, true,
-                      step + 1 < last);
+    // the records of each run of GNN_CHUNK_STEPS steps are gathered into one contiguous
+    // chunk first (stream order: after the previous run's last step), so every gradient
+    // launch reads its minibatch without dependent index loads
+    const size_t step_floats = (size_t)DDRL_MB * ua[0].lay.stride;
+    for (int step = 0; step < last; ++step) {
+      const int k = step % GNN_CHUNK_STEPS;
+      if (k == 0) launch_gnn_gather(c->stream, ua[0], step, std::min(GNN_CHUNK_STEPS, last - step), c->gnn.chunk);
+      launch_step_gnn(c->stream, ua[0], h, step, 128, 1.f / c->cfg.sgd_minibatch_size, c->gnn,
+                      c->gnn.chunk + k * step_floats);
+    }
   }
   HIPCHK(hipGetLastError());
   return 0;

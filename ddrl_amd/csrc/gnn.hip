@@ -122,7 +122,7 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
     sel = gvalid ? ga.node[graph] : 0;
   } else {
     const UpdateArgs& U = ga.u;
-    if (ga.stage) {   // staged by the previous step's reduction: no dependent index loads
+    if (ga.stage) {   // pre-gathered (launch_gnn_gather): no dependent index loads
       X = ga.stage + (size_t)(gvalid ? graph : 0) * U.lay.stride + U.lay.obs;
     } else {
       const int e = ga.step / U.nb, b = ga.step - e * U.nb;
@@ -527,17 +527,6 @@ __global__ void __launch_bounds__(256) k_gnn(GnnArgs ga) {
 }
 
 // ---- reduction over tiles: grad[p] = sum_t part[t][p] (fixed order) + norm^2 partials ----
-// Gather of the records of step `step` (rows table) into the stage, one float per thread.
-__device__ __forceinline__ float gnn_stage_load(const GnnArgs& ga, int step, int gid, int& dst) {
-  const UpdateArgs& U = ga.u;
-  const int stride = U.lay.stride;
-  dst = -1;
-  if (gid >= DDRL_MB * stride) return 0.f;
-  const int row = gid / stride, col = gid - row * stride;
-  dst = gid;
-  return U.rec[(size_t)ga.rows[(size_t)step * DDRL_MB + row] * stride + col];
-}
-
 __global__ void __launch_bounds__(256) k_gnn_reduce(GnnArgs ga, int ntiles, int n) {
   __shared__ float red[4];
   const int p = blockIdx.x * 256 + threadIdx.x;
@@ -547,20 +536,10 @@ __global__ void __launch_bounds__(256) k_gnn_reduce(GnnArgs ga, int ntiles, int 
 #pragma unroll
   for (int t = 0; t < DDRL_MB / 4; ++t)
     v[t] = (p < n && t < ntiles) ? ga.part[(size_t)t * ga.part_stride + p] : 0.f;
-  // the next step's records -> stage (this step's gradient kernel has finished reading it);
-  // issued after the partial loads, so its dependent row-table -> record chain waits behind
-  // them instead of holding them back
-  int sdst = -1;
-#ifdef DDRL_ABL_GNN_NO_STAGE_NEXT   // ablation build (timing only)
-  const float sv_next = 0.f;
-#else
-  const float sv_next = ga.stage_next ? gnn_stage_load(ga, ga.step + 1, p, sdst) : 0.f;
-#endif
   float s = 0.f;
 #pragma unroll
   for (int t = 0; t < DDRL_MB / 4; ++t) s += v[t];
   if (p < n) ga.grad[p] = s;
-  if (sdst >= 0) ga.stage[sdst] = sv_next;
   float ss = wave_sum(s * s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
   __syncthreads();
@@ -638,27 +617,24 @@ done:
   U.theta[p] = th0 - (mi * alpha) / (sqrtf(vi) + h.eps);
 }
 
-// Row table of the schedule: rows[s][i] = shuffle[perm[e][b] * 128 + i], s = e * nb + b.
-__global__ void k_gnn_rows(UpdateArgs u, int n_steps, int32_t* rows) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (size_t)n_steps * DDRL_MB) return;
-  const int s = (int)(i / DDRL_MB), r = (int)(i - (size_t)s * DDRL_MB);
-  const int e = s / u.nb, b = s - e * u.nb;
-  rows[i] = u.shuffle[u.perm[e * u.nb + b] * DDRL_MB + r];
+// Pre-gather of a run of minibatch steps: dst[k][i][col] = rec[shuffle[perm[e][b] * 128 + i]][col]
+// for step0 + k = e * nb + b.  One float per thread (the row index loads hit L2 / MALL: 128
+// rows share one perm entry, 'stride' floats share one row index).
+__global__ void k_gnn_gather(UpdateArgs u, int step0, size_t n, float* dst) {
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= n) return;
+  const int stride = u.lay.stride;
+  const size_t rowg = gid / stride;
+  const int col = (int)(gid - rowg * stride);
+  const int k = (int)(rowg / DDRL_MB), i = (int)(rowg - (size_t)k * DDRL_MB);
+  const int s = step0 + k, e = s / u.nb, b = s - e * u.nb;
+  const int row = u.shuffle[(size_t)u.perm[e * u.nb + b] * DDRL_MB + i];
+  dst[gid] = u.rec[(size_t)row * stride + col];
 }
 
-__global__ void k_gnn_stage(GnnArgs ga, int step) {
-  int dst;
-  const float v = gnn_stage_load(ga, step, blockIdx.x * blockDim.x + threadIdx.x, dst);
-  if (dst >= 0) ga.stage[dst] = v;
-}
-
-void launch_gnn_schedule(hipStream_t s, const UpdateArgs& u, int n_steps, int step0, const GnnScratch& sc) {
-  const size_t n = (size_t)n_steps * DDRL_MB;
-  hipLaunchKernelGGL(k_gnn_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, u, n_steps, sc.rows);
-  GnnArgs ga{};
-  ga.u = u; ga.rows = sc.rows; ga.stage = sc.stage;
-  hipLaunchKernelGGL(k_gnn_stage, dim3((DDRL_MB * u.lay.stride + 255) / 256), dim3(256), 0, s, ga, step0);
+void launch_gnn_gather(hipStream_t s, const UpdateArgs& u, int step0, int n_steps, float* dst) {
+  const size_t n = (size_t)n_steps * DDRL_MB * u.lay.stride;
+  hipLaunchKernelGGL(k_gnn_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, u, step0, n, dst);
 }
 
 int gnn_param_total(int A) { return gnn_net_off(A, 1).bout + 1; }
@@ -694,15 +670,13 @@ void launch_forward_gnn(hipStream_t s, const ForwardArgs& fa) {
 }
 
 void launch_step_gnn(hipStream_t s, const UpdateArgs& u, const UpdateHyper& h, int step, int nrows, float inv_n,
-                     const GnnScratch& sc, bool staged, bool stage_next) {
+                     const GnnScratch& sc, const float* stage) {
   check_a(u.A);
   GnnArgs ga{};
   ga.theta = u.theta; ga.u = u; ga.h = h; ga.step = step; ga.n_graphs = nrows; ga.inv_n = inv_n;
   ga.part = sc.part; ga.part_stride = sc.part_stride; ga.statp = sc.statp; ga.normp = sc.normp;
   ga.bp_cur = sc.bp_cur; ga.grad = u.grad_out ? u.grad_out : sc.grad;
-  if (staged) {
-    ga.stage = sc.stage; ga.rows = sc.rows; ga.stage_next = stage_next ? 1 : 0;
-  }
+  ga.stage = stage;
   const int ntiles = (nrows + 3) / 4;
   const int n = gnn_param_total(u.A);
   // tiles of the critic write their statistics after the actor's: statp [2][32][8]

@@ -173,20 +173,20 @@ struct GnnArgs {
   float* bp_cur;                 // [2] beta powers of the current step
   float* grad;                   // reduced gradient (scratch or the DDP output)
   int act_e0, act_nfull;          // act: first env of the range, envs of the shard (record rows)
-  // staged minibatch (fused update only): the records of this step, gathered by the previous
-  // step's reduction ([128][stride]); rows = the row table [steps][128] of the schedule
-  float* stage; const int32_t* rows; int stage_next;
+  // staged minibatch (fused update only): the records of this step, contiguous [128][stride]
+  // (a slot of the pre-gathered chunk); null: gather through shuffle / perm
+  const float* stage;
 };
 struct GnnScratch {
   float* part; int part_stride; float* statp; float* normp; float* bp_cur; float* grad;
-  float* stage;       // [128][stride] records of the next minibatch step
-  int32_t* rows;      // [num_sgd_iter * nb][128] record row of every (step, minibatch row)
-  size_t rows_cap;    // entries of rows
+  float* chunk;       // [GNN_CHUNK_STEPS][128][stride] records of a run of minibatch steps
 };
+#define GNN_CHUNK_STEPS 1024
 int gnn_param_total(int A);
-// staged: the fused update's schedule (rows table + staged records, see gnn.hip); false for the
-// data-parallel gradient of explicit rows
+// stage: the step's pre-gathered records (fused update) or null (data-parallel gradient of
+// explicit rows)
 void launch_step_gnn(hipStream_t s, const UpdateArgs& u, const UpdateHyper& h, int step, int nrows, float inv_n,
-                     const GnnScratch& sc, bool staged = false, bool stage_next = false);
-// the row table of a whole schedule (steps [0, n_steps)) and the staged records of step0
-void launch_gnn_schedule(hipStream_t s, const UpdateArgs& u, int n_steps, int step0, const GnnScratch& sc);
+                     const GnnScratch& sc, const float* stage = nullptr);
+// the records of minibatch steps [step0, step0 + n_steps) of the schedule -> dst
+// ([n_steps][128][stride], n_steps <= GNN_CHUNK_STEPS): one bandwidth-bound gather per chunk
+void launch_gnn_gather(hipStream_t s, const UpdateArgs& u, int step0, int n_steps, float* dst);
