@@ -535,8 +535,44 @@ __global__ void __launch_bounds__(256) k_gnn(GnnArgs ga) {
 }
 
 // ---- reduction over tiles: grad[p] = sum_t part[t][p] (fixed order) + norm^2 partials ----
+// loss statistics of the step: statp [net][tile][8]; lane j < 10 sums (net, stat) j over the
+// tiles (independent loads), lane 0 combines
+__device__ __forceinline__ void gnn_step_stats(const GnnArgs& ga, int ntiles) {
+  __shared__ float sv[10];
+  const int j = threadIdx.x, b = j / 5, k = j - 5 * b;
+  float sv_t[DDRL_MB / 4];
+#pragma unroll
+  for (int t = 0; t < DDRL_MB / 4; ++t) sv_t[t] = t < ntiles ? ga.statp[(b * DDRL_MB / 4 + t) * 8 + k] : 0.f;
+  float a = 0.f;
+#pragma unroll
+  for (int t = 0; t < DDRL_MB / 4; ++t) a += sv_t[t];
+  sv[j] = a;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  const UpdateArgs& U = ga.u;
+  if (j == 0) {
+    ga.bp_cur[0] = U.beta_pow[0];
+    ga.bp_cur[1] = U.beta_pow[1];
+    if (U.stats) {
+      const float nr = (float)ga.n_graphs;
+      float* so = U.stats + (size_t)ga.step * 8;
+      so[1] = sv[0] / nr; so[3] = sv[1] / nr; so[4] = sv[2] / nr;
+      so[2] = sv[5] / nr;
+      const float vy = sv[7] / nr - (sv[6] / nr) * (sv[6] / nr);
+      const float vd = sv[9] / nr - (sv[8] / nr) * (sv[8] / nr);
+      so[5] = vy > 0.f ? fmaxf(-1.f, 1.f - vd / vy) : 0.f;
+    }
+  }
+}
+
+// The last block of the grid (one past the parameter blocks) sums the step's loss statistics
+// instead, in parallel with the parameter blocks (not after block 0's parameters).
 __global__ void __launch_bounds__(256) k_gnn_reduce(GnnArgs ga, int ntiles, int n) {
   __shared__ float red[4];
+  if (blockIdx.x == gridDim.x - 1) {
+    if (threadIdx.x < 10) gnn_step_stats(ga, ntiles);
+    return;
+  }
   const int p = blockIdx.x * 256 + threadIdx.x;
   // all tile partials of this parameter in flight at once (a runtime-bound loop would wait
   // for each load before the next add), then summed in tile order
@@ -552,35 +588,6 @@ __global__ void __launch_bounds__(256) k_gnn_reduce(GnnArgs ga, int ntiles, int 
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
   __syncthreads();
   if (threadIdx.x == 0) ga.normp[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
-  if (blockIdx.x == 0 && threadIdx.x >= 64 && threadIdx.x < 64 + 10) {
-    // loss statistics of the step: statp [net][tile][8]; lane j of wave 1 sums (net, stat)
-    // j over the tiles (independent loads), lane 64 combines
-    __shared__ float sv[10];
-    const int j = threadIdx.x - 64, b = j / 5, k = j - 5 * b;
-    float sv_t[DDRL_MB / 4];
-#pragma unroll
-    for (int t = 0; t < DDRL_MB / 4; ++t) sv_t[t] = t < ntiles ? ga.statp[(b * DDRL_MB / 4 + t) * 8 + k] : 0.f;
-    float a = 0.f;
-#pragma unroll
-    for (int t = 0; t < DDRL_MB / 4; ++t) a += sv_t[t];
-    sv[j] = a;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    const UpdateArgs& U = ga.u;
-    if (j == 0) {
-      ga.bp_cur[0] = U.beta_pow[0];
-      ga.bp_cur[1] = U.beta_pow[1];
-      if (U.stats) {
-        const float nr = (float)ga.n_graphs;
-        float* so = U.stats + (size_t)ga.step * 8;
-        so[1] = sv[0] / nr; so[3] = sv[1] / nr; so[4] = sv[2] / nr;
-        so[2] = sv[5] / nr;
-        const float vy = sv[7] / nr - (sv[6] / nr) * (sv[6] / nr);
-        const float vd = sv[9] / nr - (sv[8] / nr) * (sv[8] / nr);
-        so[5] = vy > 0.f ? fmaxf(-1.f, 1.f - vd / vy) : 0.f;
-      }
-    }
-  }
 }
 
 // ---- tf.clip_by_global_norm + tf1 Adam over all parameters of the policy ----
@@ -693,6 +700,6 @@ void launch_step_gnn(hipStream_t s, const UpdateArgs& u, const UpdateHyper& h, i
 #ifdef DDRL_ABL_GNN_GRAD_ONLY   // ablation build (timing only): no reduction / Adam launches
   return;
 #endif
-  hipLaunchKernelGGL(k_gnn_reduce, dim3(nred), dim3(256), 0, s, ga, ntiles, n);
+  hipLaunchKernelGGL(k_gnn_reduce, dim3(nred + 1), dim3(256), 0, s, ga, ntiles, n);
   if (!u.grad_out) hipLaunchKernelGGL(k_gnn_adam, dim3(nred), dim3(256), 0, s, ga, nred, n);
 }
