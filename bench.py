@@ -358,7 +358,8 @@ def main():
     ks1 = (d + 3) // 4
     if gnn:
         kernel = "k_gnn<GRAD> + k_gnn_reduce + k_gnn_adam (three launches per minibatch step)"
-        active_cus = 2 * ((rows_per_step + 3) // 4)
+        # (tiles of 4 graphs) x (actor, critic) x 4 backward shares (gnn.hip GNN_Z), one per CU
+        active_cus = min(256, 2 * ((rows_per_step + 3) // 4) * 4)
         model = f"shared GraphNet/MPNN leg policy (4 nodes x 19 features + ego quaternion, A={A})"
     else:
         coll = "RCCL" if backend == "nccl" else backend

@@ -8,7 +8,8 @@ Per workload the bytes of every update-kernel dispatch are summed and divided by
 minibatch steps they cover:
   local: one fused k_update_ffn launch = 10 epochs x 6400 steps x 4 policies (4096 envs)
   c4:    one fused launch = 10 x 25600 steps x 1 policy (SharedDecentral, 4096 envs)
-  c5:    k_gnn<2, 2> + k_gnn_reduce + k_gnn_adam per step, 10 x 800 steps (128 envs)
+  c5:    k_gnn<2, 2> + k_gnn_reduce + k_gnn_adam per step (+ k_gnn_gather per 1024 steps),
+         10 x 800 steps (128 envs)
 """
 import csv, json, os, sys
 
@@ -18,8 +19,9 @@ WORKLOADS = {
               "workload": "QuantrupedMultiEnv_Local, 4096 envs, T=200 (one fused launch: 10 x 6400 steps x 4 policies)"},
     "c4": {"kernels": ["void k_update_ffn<2, 5"], "steps": 10 * 25600,
            "workload": "QuantrupedMultiEnv_SharedDecentral, 4096 envs, T=200 (one fused launch: 10 x 25600 steps)"},
-    "c5": {"kernels": ["void k_gnn<2, 2>", "k_gnn_reduce", "k_gnn_adam"], "steps": 10 * 800,
-           "workload": "QuantrupedMultiEnv_DecentralShared_Graph, 128 envs, T=200 (10 x 800 steps, 3 launches each)"},
+    "c5": {"kernels": ["void k_gnn<2, 2>", "k_gnn_reduce", "k_gnn_adam", "k_gnn_gather"], "steps": 10 * 800,
+           "workload": "QuantrupedMultiEnv_DecentralShared_Graph, 128 envs, T=200 (10 x 800 steps, 3 launches "
+                       "each, plus one record gather per 1024 steps)"},
 }
 
 
