@@ -31,8 +31,8 @@ def _filt(D, rng):
     return (1000.0, rng.normal(size=D) * 0.3, np.abs(rng.normal(size=D)) * 999.0 + 10.0)
 
 
-def _rollout(n, T, seed, head_scale):
-    ctx, cfg, inst = make_ctx(GNN_ENV, n, T)
+def _rollout(n, T, seed, head_scale, config=None):
+    ctx, cfg, inst = make_ctx(GNN_ENV, n, T, config)
     rng = np.random.default_rng(seed)
     params = init_gnn_params(ctx, seed + 1, head_scale=head_scale)
     orc, norms, a_gpu, a_orc = run_rollout(ctx, cfg, inst, params, rng, _filt(cfg.obs_full_dim, rng), T,
@@ -179,4 +179,39 @@ def test_gnn_update_long_horizon():
     for col, k in [(1, "policy_loss"), (2, "vf_loss"), (3, "kl"), (4, "entropy"), (6, "grad_gnorm")]:
         ref = np.array([s[k] for s in st64])
         assert np.all(np.abs(st[:, col] - ref) <= 1e-4 * np.abs(ref) + 1e-6), k
+    ctx.close()
+
+
+def test_gnn_update_across_record_chunks():
+    """The fused GNN update gathers the records of each run of 1024 minibatch steps into one
+    chunk (k_gnn_gather, GNN_CHUNK_STEPS).  A 1,030-step schedule (103 epochs of a 1,280-row
+    batch) at lr = 0 keeps the weights fixed, so every step's learner statistics are the loss
+    of its own minibatch at the initial weights: steps on both sides of the chunk boundary
+    are compared with the oracle one by one (no trajectory drift), and the weights must come
+    back unchanged bit for bit."""
+    import torch
+    ctx, cfg, orc, norms, params, _, _ = _rollout(32, 10, 71, head_scale=1.0,
+                                                  config={"num_sgd_iter": 103, "lr": 0.0})
+    lay = ctx.layout[0]
+    rec = orc.flat_records(0, lay)
+    ctx.records_set(0, rec)
+    ctx.adv_norm_set(0, *norms[0])
+    sh, pe = O.sgd_schedule(np.random.default_rng(9), rec.shape[0], 128, cfg.num_sgd_iter)
+    nb = rec.shape[0] // 128
+    steps = cfg.num_sgd_iter * nb
+    assert steps == 1030
+    p0 = ctx.params_get(0).copy()
+    ctx.ppo_update(1, [torch.from_numpy(sh).cuda()], [torch.from_numpy(pe).cuda()], [0.2])
+    ctx.synchronize()
+    np.testing.assert_array_equal(ctx.params_get(0), p0)
+    st = ctx.ppo_stats(0, steps)
+    batch = _batch(rec, lay, norms[0])
+    for k in [0, 1, 1022, 1023, 1024, 1025, 1029]:
+        e, b = divmod(k, nb)
+        _, stats = O.ppo_update("gnn", params, SHAPES, O.Adam(ctx.n_params[0], lr=0.0), batch, sh,
+                                pe[e:e + 1, b:b + 1], np.float32(0.2), {"entropy_coeff": 0.0}, steps=1)
+        s0 = stats[0]
+        ref = [s0["total_loss"], s0["policy_loss"], s0["vf_loss"], s0["kl"], s0["entropy"], s0["vf_explained_var"],
+               s0["grad_gnorm"]]
+        _close(st[k, :7], np.array(ref, np.float32), rtol=1e-4, atol=1e-5, msg=f"stats step {k}")
     ctx.close()
