@@ -397,17 +397,19 @@ __device__ __forceinline__ void xchg_store(unsigned long long* g, unsigned long 
 __device__ __forceinline__ unsigned long long xchg_load(unsigned long long* g) {
   return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-template <int NP>
-__device__ __forceinline__ void gx_get(gx_box_t r, unsigned tag, float* out, int* err) {
+template <int NP, typename F>
+__device__ __forceinline__ void gx_get(gx_box_t r, unsigned tag, float* out, int* err, F&& after_first) {
   unsigned long long g[2 * NP];
   unsigned long long* b = r + 2 * (int)threadIdx.x;
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  bool first = true;
   for (;;) {
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
       g[2 * j] = __hip_atomic_load(b + 512 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       g[2 * j + 1] = __hip_atomic_load(b + 512 * j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (first) { after_first(); first = false; }
     bool ok = true;
 #pragma unroll
     for (int j = 0; j < 2 * NP; ++j) ok = ok && (unsigned)(g[j] >> 32) == tag;
@@ -449,14 +451,16 @@ __device__ __forceinline__ unsigned long long xchg_load(unsigned long long* g) {
 }
 // The partner's NP pairs of this lane: all loads in flight, re-polled until every tag
 // matches; bounded (a timeout flags err and returns zeros).
-template <int NP>
-__device__ __forceinline__ void gx_get(gx_box_t r, unsigned tag, float* out, int* err) {
+template <int NP, typename F>
+__device__ __forceinline__ void gx_get(gx_box_t r, unsigned tag, float* out, int* err, F&& after_first) {
   v4u g[NP];
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  bool first = true;
   for (;;) {
     xchg_inv_l1();
 #pragma unroll
     for (int j = 0; j < NP; ++j) g[j] = __builtin_amdgcn_raw_buffer_load_b128(r, (j * 256 + (int)threadIdx.x) * 16, 0, DDRL_GX_LD);
+    if (first) { after_first(); first = false; }
     bool ok = true;
 #pragma unroll
     for (int j = 0; j < NP; ++j) ok = ok && g[j][1] == tag && g[j][3] == tag;
@@ -771,8 +775,9 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     STAMP(8);
     // ---- prefetch: the records of step + 1 land in stg (LDS-DMA) while the dW1 tiles, the
     //      norm exchange and Adam run; every lane has read its rows of this step (sync #1).
-    //      The row split issues them after its partner exchange instead: vmcnt retires in
-    //      order, so the exchange loads would otherwise wait for the gathers.
+    //      The row split issues them with its partner exchange instead, behind the first
+    //      poll's loads: vmcnt retires in order, so the exchange loads would otherwise wait
+    //      for the gathers.
 #ifndef DDRL_ABL_NO_PREFETCH
     if (KSP == 1 && step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, idxb, stg, U.R, ub.lds_bytes);
 #endif
@@ -810,7 +815,16 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
         gx_put(gx_mine, NP0 + 2 * i + 1, gt[i][2], gt[i][3], gtag, coh);
       }
       float o[2 * NP];
-      gx_get<NP>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), gtag, o, ub.err);
+#ifndef DDRL_ABL_NO_PREFETCH
+      // the next step's record gathers go out right behind the first poll's loads (which
+      // retire first: vmcnt is in order; a re-poll then waits for them too): 13.0 -> 12.9 us
+      // per step against issuing them after the exchange
+      gx_get<NP>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), gtag, o, ub.err, [&] {
+        if (step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, idxb, stg, U.R, ub.lds_bytes);
+      });
+#else
+      gx_get<NP>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), gtag, o, ub.err, [] {});
+#endif
 #pragma unroll
       for (int k = 0; k < NSLOT; ++k) gs[k] += o[k];
       if (tid < NSTAT) red[96 + tid] = st_own + o[NSLOT];
@@ -818,9 +832,6 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       for (int i = 0; i < NTS; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) gt[i][r] += o[2 * NP0 + 4 * i + r];
-#ifndef DDRL_ABL_NO_PREFETCH
-      if (step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, idxb, stg, U.R, ub.lds_bytes);
-#endif
       STAMP(14);
     } else {
 #pragma unroll
