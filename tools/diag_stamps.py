@@ -6,13 +6,22 @@ import numpy as np, torch
 from ddrl_amd import build, native as N
 extra = os.environ.get("DDRL_EXTRA_FLAGS", "").split()
 tag = "".join(ch for ch in "".join(extra) if ch.isalnum())[:24]
-lib = build.build(extra_flags=["-DDDRL_STAMPS"] + extra,
-                  lib=os.path.join(os.path.dirname(N.LIB_PATH), f"libddrl_hip_diag{tag}.so"),
-                  build_dir=os.path.join(os.path.dirname(N.LIB_PATH), f"_build_diag{tag}"))
+# prebuilt (here, on the CPU) when DDRL_STAMPS_LIB names it: python tools/diag_stamps.py --build
+stamps_lib = os.path.join(os.path.dirname(N.LIB_PATH), "libddrl_hip_stamps.so")
+if "--build" in sys.argv or not os.environ.get("DDRL_STAMPS_LIB"):
+    lib = build.build(extra_flags=["-DDDRL_STAMPS"] + extra,
+                      lib=stamps_lib if "--build" in sys.argv else
+                      os.path.join(os.path.dirname(N.LIB_PATH), f"libddrl_hip_diag{tag}.so"),
+                      build_dir=os.path.join(os.path.dirname(N.LIB_PATH), f"_build_diag{tag}"))
+    if "--build" in sys.argv:
+        print(lib)
+        sys.exit(0)
+else:
+    lib = stamps_lib
 N.load(lib)
 from ddrl_amd.spec import make_cfg
 from ddrl_amd.trainer import glorot_ffn_flat
-n, T = int(sys.argv[1]) if len(sys.argv) > 1 else 512, 200
+n, T = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 512, 200
 cfg, inst = make_cfg("QuantrupedMultiEnv_Local", n, T)
 ctx = N.Context(cfg, 0, torch.cuda.current_stream().cuda_stream)
 rng = np.random.default_rng(0)
