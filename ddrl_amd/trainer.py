@@ -215,6 +215,7 @@ class PPOTrainer:
         self.iteration += 1
         cb = self.config.get("callbacks", {}).get("on_train_result") if isinstance(
             self.config.get("callbacks"), dict) else None
+        self.last_learner = learner
         result = {"training_iteration": self.iteration, "timesteps_total": self.timesteps_total,
                   "timesteps_this_iter": steps, "info": {"learner": learner},
                   "timers": {"sample_time_ms": (t1 - t0) * 1e3, "learn_time_ms": (t2 - t1) * 1e3,
@@ -280,6 +281,49 @@ class PPOTrainer:
         from .rllib_checkpoint import policy_ids, policy_state, read_checkpoint
         ck = read_checkpoint(path)
         return self.load_policy_states({pid: policy_state(ck, pid) for pid in policy_ids(ck)})
+
+    def rllib_policy_states(self):
+        """Per policy id the state rllib_checkpoint.worker_tree writes: Keras-order weights,
+        Adam m / v, beta powers, the RLlib MeanStdFilter RunningStat (when this trainer runs
+        observation_filter = MeanStdFilter; NoFilter otherwise) and the variable shapes."""
+        from .rllib_checkpoint import ffn_shapes, gnn_shapes
+        out = {}
+        A = self.cfg.act_dim
+        for p, pid in enumerate(self.policy_ids):
+            m, v, b1, b2 = self.ctx.adam_get(p)
+            d = int(self.cfg.obs_dim[p])
+            if self.cfg.model_kind == N.MODEL_FFN:
+                shapes = ffn_shapes(d, 2 * A) + ([("leg_coupling", (4, A))] if self.cfg.leg_coupling else [])
+            else:
+                shapes = gnn_shapes(2 * A)
+            st = {"weights": self.ctx.params_get(p), "adam_m": m, "adam_v": v,
+                  "beta_powers": (np.float32(b1), np.float32(b2)), "shapes": shapes, "obs_dim": d,
+                  "filter": None, "filter_buffer": None}
+            if self.cfg.policy_filter:
+                st["filter"] = self.ctx.policy_filter_get(p)
+            else:
+                st["filter_kind"] = "NoFilter"
+            out[pid] = st
+        return {pid: out[pid] for pid in sorted(out)}   # Ray 1.0.1 writes the policies sorted by id
+
+    def save_rllib(self, checkpoint_dir, time_total=0.0, episodes_total=0):
+        """Write an RLlib (Ray 1.0.1) checkpoint of this trainer --
+        <checkpoint_dir>/checkpoint_<i>/checkpoint-<i> + .tune_metadata -- in the layout
+        PPOTrainer.restore reads (evaluation/evaluate_trained_policies_pd.py:93-96), with the
+        learner statistics of the last train() call.  The writer emits the pickle opcodes
+        itself (ddrl_amd.rllib_checkpoint.emit); it reproduces every published checkpoint
+        byte for byte from its contents (tests/test_checkpoint.py)."""
+        from .rllib_checkpoint import write_checkpoint
+        last = getattr(self, "last_learner", {}) or {}
+        learner = {}
+        for p, pid in enumerate(self.policy_ids):
+            s = dict(last.get(pid, {}))
+            s.setdefault("cur_kl_coeff", float(np.float32(self.kl_coeff[p])))
+            s.setdefault("cur_lr", float(np.float32(self.cfg.lr)))
+            s.setdefault("entropy_coeff", float(self.cfg.entropy_coeff))
+            learner[pid] = s
+        return write_checkpoint(checkpoint_dir, self.iteration, self.rllib_policy_states(), learner,
+                                self.timesteps_total, time_total=time_total, episodes_total=episodes_total)
 
     def load_policy_states(self, states):
         """Per policy id: {"weights", "adam_m", "adam_v", "beta_powers", "filter" (n, M, S) or

@@ -6,7 +6,8 @@ per policy the Keras-order weights, Adam m / v, beta powers, the RLlib MeanStdFi
 (n, M, S) and the KL coefficient, plus the variable / optimizer-slot order and shapes of one
 checkpoint of every published architecture (JSON).
 
-    python tests/golden/make_checkpoint_fixture.py     # in the container (needs /root/reference)
+    python tests/golden/make_checkpoint_fixture.py            # in the container (needs /root/reference)
+    python tests/golden/make_checkpoint_fixture.py --digest   # + ckpt_local_1250_digest.json (writer test)
 """
 import glob
 import json
@@ -56,5 +57,31 @@ def main():
     print("wrote ckpt_local_1250.npz and ckpt_layouts.json for", len(orders), "architectures")
 
 
+def digests():
+    """ckpt_local_1250_digest.json: what the writer test needs besides the npz to rebuild the
+    published Local checkpoint byte for byte -- the SHA-256 of checkpoint-1250 and of its
+    .tune_metadata, the metadata fields, the trainer counters and the (empty) filter buffers."""
+    import hashlib
+    from ddrl_amd.rllib_checkpoint import to_data, walk
+    path = os.path.join(REF, LOCAL)
+    ck = read_checkpoint(path)
+    raw = open(path, "rb").read()
+    md_raw = open(path + ".tune_metadata", "rb").read()
+    buffers = {}
+    for pid in policy_ids(ck):
+        b = ck["worker"]["filters"][pid]["state"]["buffer"]["state"]
+        assert b["_n"] == 0 and not np.any(b["_M"]) and not np.any(b["_S"])
+        buffers[pid] = {"n": 0, "width": int(b["_M"].shape[0])}
+    out = {"source": LOCAL, "sha256": hashlib.sha256(raw).hexdigest(), "bytes": len(raw),
+           "metadata_sha256": hashlib.sha256(md_raw).hexdigest(), "metadata": to_data(walk(md_raw)),
+           "counters": ck["train_exec_impl"]["counters"], "filter_buffers": buffers}
+    with open(os.path.join(HERE, "ckpt_local_1250_digest.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    print("wrote ckpt_local_1250_digest.json")
+
+
 if __name__ == "__main__":
-    main()
+    if "--digest" in sys.argv:
+        digests()
+    else:
+        main()
