@@ -112,6 +112,15 @@ class HipBackend:
     def stats(self, pid, n):
         return self.ctx.ppo_stats(pid, n)
 
+    def snapshot(self, pid):
+        """Weights, Adam m / v and beta powers of the policy (restored if the update fails)."""
+        return self.ctx.params_get(pid), self.ctx.adam_get(pid)
+
+    def restore(self, pid, snap):
+        theta, (m, v, b1, b2) = snap
+        self.ctx.params_set(pid, theta)
+        self.ctx.adam_set(pid, m, v, b1, b2)
+
 
 def native_comm_init(ctx, comm):
     """Give the C-ABI context its own RCCL communicator over the ranks of `comm`: rank 0 makes
@@ -157,30 +166,47 @@ class DataParallelLearner:
         Returns the all-reduced mean KL of the last epoch."""
         E, nb = perms.shape
         m = self.rows_per_rank
+        snap = self.backend.snapshot(self.pid) if hasattr(self.backend, "snapshot") else None
+        err = None
         for e in range(E):
             last = e == E - 1
             for b in range(nb):
                 s = int(perms[e, b]) * m
-                self.backend.grad(self.pid, shuffle[s:s + m], m, kl_coeff, grad, b if last else -1)
+                if err is None:
+                    try:
+                        self.backend.grad(self.pid, shuffle[s:s + m], m, kl_coeff, grad, b if last else -1)
+                    except Exception as ex:   # DdrlError of a failed launch: stop computing,
+                        err = ex              # keep joining the collectives (zero contribution)
+                if err is not None:
+                    grad.zero_()
                 self.comm.all_reduce_(grad)
                 if self.grad_scale != 1.0:
                     grad.mul_(self.grad_scale)
-                self.backend.apply(self.pid, grad)
-        return self._kl(nb)
+                if err is None:
+                    try:
+                        self.backend.apply(self.pid, grad)
+                    except Exception as ex:
+                        err = ex
+        return self._kl(nb, err, snap)
 
-    def _kl(self, nb):
+    def _kl(self, nb, err=None, snap=None):
         """All-reduced mean KL of the last epoch.  The error state of every rank is exchanged
-        first (max of a flag): a rank whose update kernel reported an error (norm-exchange
-        timeout) makes every rank raise, instead of the others blocking in their next
-        collective while it unwinds."""
-        err = None
-        try:
-            st = self.backend.stats(self.pid, nb)
-            kl_local = float(np.mean(st[:, 3].astype(np.float64)))
-        except Exception as e:   # the backend's own error (DdrlError from the C-ABI)
-            err, kl_local = e, 0.0
+        first (max of a flag): a rank whose gradient / apply launch or update kernel reported
+        an error (e.g. an exchange timeout) makes every rank raise, instead of the others
+        blocking in their next collective while it unwinds.  A failing rank keeps joining
+        every step's all-reduce with a zero gradient, and on failure every rank restores the
+        weights / Adam state it held before the update (`snap`), so they stay identical."""
+        kl_local = 0.0
+        if err is None:
+            try:
+                st = self.backend.stats(self.pid, nb)
+                kl_local = float(np.mean(st[:, 3].astype(np.float64)))
+            except Exception as e:   # the backend's own error (DdrlError from the C-ABI)
+                err = e
         red = self.comm.all_reduce_np(np.array([kl_local, 1.0 if err is not None else 0.0]))
         if red[1] > 0:
+            if snap is not None:
+                self.backend.restore(self.pid, snap)
             if err is not None:
                 raise err
             raise RuntimeError(f"data-parallel update failed on {int(red[1])} other rank(s)")

@@ -34,6 +34,12 @@ class HostMultiAgentEnv:
         self.n = int(n_envs)
         self.D = len(self.spec.obs_fields)
         tv = self.spec.target_velocity_list
+        if tv and len(set(float(v) for v in tv)) > 1:
+            # the reference draws random.choice(target_velocity_list) on every reset
+            # (quantruped_adaptor_multi_environment.py:50, :216); the host env plane holds one
+            # target velocity for all envs, so a list of several is refused, not truncated
+            raise ValueError(f"target_velocity {list(tv)}: the host env plane supports one target velocity "
+                             "(the reference re-draws from the list on every reset)")
         self.env = N.HostEnv(self.n, self.D, n_threads, seed, float(tv[0]) if tv else 0.0)
         self.clip = filter_clip
         # env-side MeanStdFilter singleton: RunningStat (n, M, S), fp64

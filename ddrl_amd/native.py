@@ -424,16 +424,28 @@ class HostEnv:
         if rc != 0:
             raise DdrlError(self.lib.ddrl_hostenv_last_error().decode())
 
+    def _live(self):
+        if not getattr(self, "h", None):
+            raise DdrlError("host env plane is closed")
+
     def reset(self):
+        """Reset every env; returns a COPY of the observations (self.obs is the live pinned
+        buffer that the next step() overwrites in place)."""
+        self._live()
         self._ck(self.lib.ddrl_hostenv_reset(self.h))
-        return self.obs
+        return self.obs.copy()
 
     def step(self, e0=0, e1=None):
         """Step the envs [e0, e1) with the actions in self.act (written by the caller)."""
+        self._live()
         self._ck(self.lib.ddrl_hostenv_step(self.h, e0, self.n if e1 is None else e1))
 
     def close(self):
+        """Free the pinned buffers.  The numpy views over them are dropped first (set to None),
+        so no attribute of this object can read freed memory afterwards; copies made by the
+        caller stay valid."""
         if getattr(self, "h", None):
+            self.obs = self.act = self.fw = self.cfrc = self.done = None
             self.lib.ddrl_hostenv_destroy(self.h)
             self.h = None
 

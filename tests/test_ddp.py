@@ -271,26 +271,40 @@ def test_native_comm_init_broadcasts_rank0_id_world2():
 
 
 class _FailingBackend:
-    """Gradient / apply do nothing; stats raise on the failing rank, as ddrl_ppo_stats does
-    when the update kernel's error word is set (norm-exchange timeout)."""
+    """Gradient adds 1 to every entry, apply adds the all-reduced gradient to a weight vector;
+    on the failing rank `where` ("stats" | "grad" | "apply") raises, as ddrl_ppo_stats does
+    when the update kernel's error word is set (exchange timeout) or a launch fails."""
 
-    def __init__(self, fail):
-        self.fail = fail
+    def __init__(self, fail, where="stats"):
+        self.fail, self.where, self.calls = fail, where, 0
+        self.theta = np.zeros(4)
+
+    def _maybe(self, what):
+        self.calls += 1
+        if self.fail and self.where == what and (what == "stats" or self.calls >= 3):
+            from ddrl_amd.native import DdrlError
+            raise DdrlError(f"update kernel: {what} failed (exchange timed out)")
 
     def grad(self, pid, rows, n_rows, kl, grad, stats_step):
-        pass
+        self._maybe("grad")
+        grad.fill_(1.0)
 
     def apply(self, pid, grad):
-        pass
+        self._maybe("apply")
+        self.theta = self.theta + grad.numpy()
 
     def stats(self, pid, n):
-        if self.fail:
-            from ddrl_amd.native import DdrlError
-            raise DdrlError("update kernel: norm exchange between the policy and value workgroups timed out")
+        self._maybe("stats")
         return np.zeros((n, 8), np.float32)
 
+    def snapshot(self, pid):
+        return self.theta.copy()
 
-def _error_worker(rank, world, port, out_dir):
+    def restore(self, pid, snap):
+        self.theta = snap.copy()
+
+
+def _error_worker(rank, world, port, out_dir, where="stats"):
     import torch
     import torch.distributed as dist
     from ddrl_amd.ddp import Comm, DataParallelLearner
@@ -298,7 +312,9 @@ def _error_worker(rank, world, port, out_dir):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     comm = Comm("cpu")
-    learner = DataParallelLearner(_FailingBackend(rank == 1), comm, 0, MB, "split")
+    be = _FailingBackend(rank == 1, where)
+    be.theta[:] = 5.0
+    learner = DataParallelLearner(be, comm, 0, MB, "split")
     grad = torch.zeros(4)
     msg = "no error"
     try:
@@ -309,18 +325,22 @@ def _error_worker(rank, world, port, out_dir):
     t = torch.ones(1)
     dist.all_reduce(t)
     with open(os.path.join(out_dir, f"e{rank}.txt"), "w") as f:
-        f.write(f"{msg}\n{float(t[0])}")
+        f.write(f"{msg}\n{float(t[0])}\n{be.theta.tolist()}")
     dist.destroy_process_group()
 
 
-def test_learner_error_raises_on_every_rank_world2():
-    """an update error on one rank (here rank 1's stats raise) makes every rank
-    raise after the learn loop (the error flag is all-reduced with the KL), and the ranks stay
-    in step for the next collective instead of one blocking while the other unwinds."""
+@pytest.mark.parametrize("where", ["stats", "grad", "apply"])
+def test_learner_error_raises_on_every_rank_world2(where):
+    """an update error on one rank -- its stats (the kernel's error word), or a
+    gradient / apply launch in the middle of the loop -- makes every rank raise after the
+    learn loop (the error flag is all-reduced with the KL; a failing rank keeps joining each
+    step's all-reduce with a zero gradient), every rank restores the weights it held before
+    the update, and the ranks stay in step for the next collective."""
     import torch.multiprocessing as mp
     out = tempfile.mkdtemp()
-    mp.spawn(_error_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    mp.spawn(_error_worker, args=(2, _free_port(), out, where), nprocs=2, join=True)
     msgs = [open(os.path.join(out, f"e{r}.txt")).read().splitlines() for r in range(2)]
     assert msgs[1][0].startswith("DdrlError") and "timed out" in msgs[1][0]
     assert msgs[0][0].startswith("RuntimeError") and "other rank" in msgs[0][0]
     assert msgs[0][1] == msgs[1][1] == "2.0"
+    assert msgs[0][2] == msgs[1][2] == str([5.0] * 4)   # weights as before the update

@@ -283,3 +283,30 @@ def test_host_env_thread_pool_many_small_jobs():
         e.close()
     np.testing.assert_array_equal(runs[0][0], runs[1][0])
     np.testing.assert_array_equal(runs[0][1], runs[1][1])
+
+
+def test_host_env_close_drops_buffer_views_and_reset_returns_copy():
+    """after close() no attribute of the HostEnv views freed pinned memory (the
+    views are dropped first), further calls raise, and reset() hands out a copy -- not the
+    live buffer the next step() overwrites."""
+    e = N.HostEnv(4, 43, 1, seed=1)
+    o = e.reset()
+    e.act[:] = 0.5
+    e.step()
+    assert not np.array_equal(o, e.obs)      # the step changed the live buffer, not the copy
+    e.close()
+    assert e.obs is None and e.act is None and e.fw is None and e.cfrc is None and e.done is None
+    with pytest.raises(N.DdrlError):
+        e.step()
+    assert np.isfinite(o).all()              # the caller's copy stays valid
+
+
+def test_host_dict_env_refuses_several_target_velocities():
+    """the reference re-draws random.choice(target_velocity_list) on every reset
+    (quantruped_adaptor_multi_environment.py:50, :216); the host env plane holds one target
+    velocity, so a list of several distinct values is refused rather than silently truncated."""
+    from ddrl_amd.hostenv import HostMultiAgentEnv
+    with pytest.raises(ValueError, match="one target velocity"):
+        HostMultiAgentEnv("QuantrupedMultiEnv_Local", {"target_velocity": [0.5, 1.0]})
+    env = HostMultiAgentEnv("QuantrupedMultiEnv_Local", {"target_velocity": [0.75, 0.75]})
+    env.env.close()
