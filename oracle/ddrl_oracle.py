@@ -295,24 +295,41 @@ def cup_backward(p, cache, dlogits, dvalue):
 
 # --------------------------------------------------------------------------------------
 # a9 / a10  GraphNet + MPNN (models/graph_net.py:8-45, models/gcn.py:39-94,
-#           models/shared_graphnet_glorot_uniform_init.py:14-58)
+#           models/shared_graphnet_glorot_uniform_init.py:14-58); f4 alternates GCN / MPNN2 /
+#           GAT1 (models/gcn.py:7-37, 96-150, 153-206; models/graph_ops.py:3-26)
 # --------------------------------------------------------------------------------------
-def gnn_net_shapes(num_outputs, hidden=64, feat=19, qdim=4):
-    return [
-        ("state_enc/kernel", (qdim, feat * hidden)), ("state_enc/bias", (feat * hidden,)),
-        ("mpnn/msg/kernel", (hidden, hidden)), ("mpnn/node/kernel", (hidden, hidden)),
-        ("linear_out/kernel", (hidden, num_outputs)), ("linear_out/bias", (num_outputs,)),
-    ]
+# The message-passing layer of GraphNet is MPNN in the reference (graph_net.py:20); GCN, MPNN2
+# and GAT1 (gcn.py:7-37, 96-150, 153-206, with graph_ops.py:13-26) are the alternates that line
+# selects.  All four take (x [B, n, 64], adj [B, n, n]) and return tanh(...) [B, n, 64] with
+# no bias (use_bias=False, graph_net.py:22).  Edges are tf.where(adj): (batch, sender = row,
+# receiver = column).
+GNN_LAYERS = ("mpnn", "gcn", "mpnn2", "gat1")
 
 
-def gnn_param_shapes(num_outputs, hidden=64):
-    return ([("actor/" + n, s) for n, s in gnn_net_shapes(num_outputs, hidden)] +
-            [("critic/" + n, s) for n, s in gnn_net_shapes(1, hidden)])
+def gnn_layer_shapes(layer, hidden=64):
+    return {"mpnn": [("mpnn/msg/kernel", (hidden, hidden)), ("mpnn/node/kernel", (hidden, hidden))],
+            "gcn": [("gcn/linear/kernel", (hidden, hidden))],
+            "mpnn2": [("mpnn2/msg/kernel", (2 * hidden, hidden)), ("mpnn2/node/kernel", (2 * hidden, hidden))],
+            "gat1": [("gat1/pre_att/kernel", (hidden, hidden)), ("gat1/att/kernel", (2 * hidden, 1))]}[layer]
 
 
-def gnn_init(rng, num_outputs, hidden=64):
+def gnn_net_shapes(num_outputs, hidden=64, feat=19, qdim=4, layer="mpnn"):
+    return ([("state_enc/kernel", (qdim, feat * hidden)), ("state_enc/bias", (feat * hidden,))] +
+            gnn_layer_shapes(layer, hidden) +
+            [("linear_out/kernel", (hidden, num_outputs)), ("linear_out/bias", (num_outputs,))])
+
+
+def gnn_param_shapes(num_outputs, hidden=64, layer="mpnn"):
+    return ([("actor/" + n, s) for n, s in gnn_net_shapes(num_outputs, hidden, layer=layer)] +
+            [("critic/" + n, s) for n, s in gnn_net_shapes(1, hidden, layer=layer)])
+
+
+def gnn_init(rng, num_outputs, hidden=64, layer="mpnn"):
+    """GlorotUniformScaled(1.0) for the encoder and the layer kernels (GAT1 takes Keras'
+    default glorot_uniform: the same law), 0.01 for linear_out, zero biases; one draw per
+    kernel in variable order."""
     p = {}
-    for name, shape in gnn_param_shapes(num_outputs, hidden):
+    for name, shape in gnn_param_shapes(num_outputs, hidden, layer):
         if name.endswith("bias"):
             p[name] = np.zeros(shape, F32)
         else:
@@ -321,38 +338,126 @@ def gnn_init(rng, num_outputs, hidden=64):
     return p
 
 
-def _graphnet_forward(p, pre, X, node_idx, adj, hidden=64):
+def _edges(adj):
+    e = (adj != 0).astype(F32)          # e[b, s, r]: edge sender s -> receiver r
+    cnt = e.sum(1)                      # in-degree of every receiver
+    return e, cnt
+
+
+def _seg_mean(e, cnt, msg_sr):
+    """unsorted_segment_mean over receivers of per-edge messages msg_sr [B, s, r, k]."""
+    m = np.einsum("bsr,bsrj->brj", e, msg_sr)
+    return np.where(cnt[..., None] > 0, m / np.maximum(cnt[..., None], 1), 0.0).astype(F32)
+
+
+def _layer_forward(p, pre, layer, h, adj):
+    """The message-passing layer; returns y and its cache."""
+    if layer == "mpnn":             # gcn.py:57-94
+        e, cnt = _edges(adj)
+        msg = h @ p[pre + "mpnn/msg/kernel"]
+        m = np.einsum("bsr,bsj->brj", e, msg)
+        m = np.where(cnt[..., None] > 0, m / np.maximum(cnt[..., None], 1), 0.0).astype(F32)
+        y = np.tanh(h @ p[pre + "mpnn/node/kernel"] + m)
+        return y, (e, cnt)
+    if layer == "gcn":              # gcn.py:29-37 with graph_ops.adj_norm (:13-21): D^-1 A
+        an = (adj / adj.sum(-1, keepdims=True)).astype(F32)
+        hbar = an @ h
+        y = np.tanh(hbar @ p[pre + "gcn/linear/kernel"])
+        return y, (an, hbar)
+    if layer == "mpnn2":            # gcn.py:113-150: message W [x_snd | x_rec], update W [x | m]
+        e, cnt = _edges(adj)
+        n = h.shape[1]
+        hs = np.broadcast_to(h[:, :, None, :], (h.shape[0], n, n, h.shape[2]))   # sender s
+        hr = np.broadcast_to(h[:, None, :, :], (h.shape[0], n, n, h.shape[2]))   # receiver r
+        cat = np.concatenate([hs, hr], -1)
+        esr = cat @ p[pre + "mpnn2/msg/kernel"]
+        m = _seg_mean(e, cnt, esr)
+        y = np.tanh(np.concatenate([h, m], -1) @ p[pre + "mpnn2/node/kernel"])
+        return y, (e, cnt, cat, m)
+    if layer == "gat1":             # gcn.py:171-206 with graph_ops.segment_softmax (:23-26)
+        n = h.shape[1]
+        adj1 = np.minimum(F32(1), adj + np.eye(n, dtype=F32)[None])
+        e = (adj1 != 0).astype(F32)
+        z = h @ p[pre + "gat1/pre_att/kernel"]
+        a = p[pre + "gat1/att/kernel"][:, 0]
+        H = z.shape[2]
+        pre_sr = (z @ a[:H])[:, :, None] + (z @ a[H:])[:, None, :]     # concat(z_s, z_r) . a
+        lr = np.where(pre_sr > 0, pre_sr, F32(0.2) * pre_sr)           # tf.nn.leaky_relu (0.2)
+        ex = np.exp(lr) * e
+        S = ex.sum(1)                                                   # per receiver r
+        att = (ex / S[:, None, :]).astype(F32)                          # scatter_nd -> [b, s, r]
+        y = np.tanh(att @ z)                                            # x'_s = sum_r att[s, r] z_r
+        return y, (e, z, a, pre_sr, att)
+    raise ValueError(f"unknown gnn layer {layer!r}")
+
+
+def _layer_backward(p, pre, layer, h, y, cache, dy, g):
+    """Gradient of the layer's kernels into g; returns dL/dh."""
+    du = dy * (1 - y * y)
+    if layer == "mpnn":
+        e, cnt = cache
+        g[pre + "mpnn/node/kernel"] = np.einsum("bnj,bnk->jk", h, du)
+        dh = du @ p[pre + "mpnn/node/kernel"].T
+        dm = np.where(cnt[..., None] > 0, du / np.maximum(cnt[..., None], 1), 0.0)
+        dmsg = np.einsum("bsr,brj->bsj", e, dm)
+        g[pre + "mpnn/msg/kernel"] = np.einsum("bnj,bnk->jk", h, dmsg)
+        return dh + dmsg @ p[pre + "mpnn/msg/kernel"].T
+    if layer == "gcn":
+        an, hbar = cache
+        g[pre + "gcn/linear/kernel"] = np.einsum("bnj,bnk->jk", hbar, du)
+        dhbar = du @ p[pre + "gcn/linear/kernel"].T
+        return np.einsum("bsn,bsj->bnj", an, dhbar)
+    if layer == "mpnn2":
+        e, cnt, cat, m = cache
+        H = h.shape[2]
+        W = p[pre + "mpnn2/node/kernel"]
+        g[pre + "mpnn2/node/kernel"] = np.einsum("bnj,bnk->jk", np.concatenate([h, m], -1), du)
+        dcat = du @ W.T
+        dh, dm = dcat[..., :H], dcat[..., H:]
+        dm = np.where(cnt[..., None] > 0, dm / np.maximum(cnt[..., None], 1), 0.0)
+        de = e[..., None] * dm[:, None, :, :]                          # [b, s, r, k]
+        Wm = p[pre + "mpnn2/msg/kernel"]
+        g[pre + "mpnn2/msg/kernel"] = np.einsum("bsrj,bsrk->jk", cat, de)
+        dcat_e = de @ Wm.T
+        return dh + dcat_e[..., :H].sum(2) + dcat_e[..., H:].sum(1)
+    if layer == "gat1":
+        e, z, a, pre_sr, att = cache
+        H = z.shape[2]
+        datt = np.einsum("bsj,brj->bsr", du, z) * e
+        dz = np.einsum("bsr,bsj->brj", att, du)
+        colsum = (att * datt).sum(1)                                     # per receiver r
+        dex = att * (datt - colsum[:, None, :])                          # softmax over senders of r
+        dpre = dex * np.where(pre_sr > 0, F32(1), F32(0.2))
+        dps, dur = dpre.sum(2), dpre.sum(1)                              # d(z_s.a1), d(z_r.a2)
+        g[pre + "gat1/att/kernel"] = np.concatenate(
+            [np.einsum("bs,bsj->j", dps, z), np.einsum("br,brj->j", dur, z)])[:, None]
+        dz = dz + dps[..., None] * a[:H] + dur[..., None] * a[H:]
+        g[pre + "gat1/pre_att/kernel"] = np.einsum("bnj,bnk->jk", h, dz)
+        return dz @ p[pre + "gat1/pre_att/kernel"].T
+    raise ValueError(f"unknown gnn layer {layer!r}")
+
+
+def _graphnet_forward(p, pre, X, node_idx, adj, hidden=64, layer="mpnn"):
     B = X.shape[0]
     f, q = X[..., :-4], X[..., -4:]
     feat = f.shape[-1]
     wn = np.tanh(q @ p[pre + "state_enc/kernel"] + p[pre + "state_enc/bias"])
     wn = wn.reshape(B, 4, feat, hidden)
     h = np.tanh(np.einsum("bni,bnij->bnj", f, wn))
-    msg = h @ p[pre + "mpnn/msg/kernel"]
-    # unsorted_segment_mean over receivers: adj[b, s, r] != 0  (tf.where order)
-    cnt = (adj != 0).sum(1)  # [B, receivers]
-    m = np.einsum("bsr,bsj->brj", (adj != 0).astype(F32), msg)
-    m = np.where(cnt[..., None] > 0, m / np.maximum(cnt[..., None], 1), 0.0).astype(F32)
-    y = np.tanh(h @ p[pre + "mpnn/node/kernel"] + m)
+    y, lc = _layer_forward(p, pre, layer, h, adj)
     ysel = y[np.arange(B), node_idx]
     out = ysel @ p[pre + "linear_out/kernel"] + p[pre + "linear_out/bias"]
-    return out.astype(F32), (f, q, wn, h, y, ysel, cnt)
+    return out.astype(F32), (f, q, wn, h, y, ysel, lc, layer)
 
 
 def _graphnet_backward(p, pre, cache, dout, node_idx, adj, g):
-    f, q, wn, h, y, ysel, cnt = cache
+    f, q, wn, h, y, ysel, lc, layer = cache
     B = f.shape[0]
     g[pre + "linear_out/kernel"] = ysel.T @ dout
     g[pre + "linear_out/bias"] = dout.sum(0)
     dy = np.zeros_like(y)
     dy[np.arange(B), node_idx] = dout @ p[pre + "linear_out/kernel"].T
-    du = dy * (1 - y * y)
-    g[pre + "mpnn/node/kernel"] = np.einsum("bnj,bnk->jk", h, du)
-    dh = du @ p[pre + "mpnn/node/kernel"].T
-    dm = np.where(cnt[..., None] > 0, du / np.maximum(cnt[..., None], 1), 0.0)
-    dmsg = np.einsum("bsr,brj->bsj", (adj != 0).astype(F32), dm)
-    g[pre + "mpnn/msg/kernel"] = np.einsum("bnj,bnk->jk", h, dmsg)
-    dh = dh + dmsg @ p[pre + "mpnn/msg/kernel"].T
+    dh = _layer_backward(p, pre, layer, h, y, lc, dy, g)
     dz = dh * (1 - h * h)
     dwn = np.einsum("bni,bnj->bnij", f, dz)
     dpre = (dwn * (1 - wn * wn)).reshape(B, 4, -1)
@@ -360,13 +465,14 @@ def _graphnet_backward(p, pre, cache, dout, node_idx, adj, g):
     g[pre + "state_enc/bias"] = dpre.sum((0, 1))
 
 
-def gnn_forward(p, X, node_idx, adj=None):
+def gnn_forward(p, X, node_idx, adj=None, layer="mpnn"):
     X = np.asarray(X, F32)
     node_idx = np.asarray(node_idx).reshape(-1).astype(np.int64)
     if adj is None:
         adj = np.broadcast_to(ring_adjacency(), (X.shape[0], 4, 4))
-    logits, ca = _graphnet_forward(p, "actor/", X, node_idx, adj)
-    value, cc = _graphnet_forward(p, "critic/", X, node_idx, adj)
+    adj = np.asarray(adj, F32)
+    logits, ca = _graphnet_forward(p, "actor/", X, node_idx, adj, layer=layer)
+    value, cc = _graphnet_forward(p, "critic/", X, node_idx, adj, layer=layer)
     return logits, value[:, 0], (ca, cc, node_idx, adj)
 
 
@@ -591,7 +697,8 @@ def ppo_update(model, params, shapes, adam, batch, shuffle, perms, kl_coeff, cfg
             elif model == "cup":
                 logits, value, cache = cup_forward(p, batch["obs"][rows], batch["leg"][rows])
             else:
-                logits, value, cache = gnn_forward(p, batch["X"][rows], batch["node_idx"][rows])
+                logits, value, cache = gnn_forward(p, batch["X"][rows], batch["node_idx"][rows],
+                                                   layer=cfg.get("gnn_layer", "mpnn"))
             dlogits, dvalue, st = ppo_loss_rows(
                 logits, value, batch["actions"][rows], batch["logits"][rows],
                 batch["logp"][rows], batch["vf_preds"][rows], batch["adv"][rows],

@@ -221,6 +221,89 @@ def test_gnn_gradients_match_autograd():
         np.testing.assert_allclose(g[k], ref, rtol=1e-4, atol=2e-5 * np.abs(ref).max(), err_msg=k)
 
 
+def _torch_gnn_layer(layer, t, pre, x, adj):
+    """The reference's layer call (models/gcn.py), literally: tf.where edge lists, gather_nd,
+    unsorted_segment_mean / segment_softmax, scatter_nd -- written in torch, independent of the
+    oracle's einsum formulation."""
+    B, n, H = x.shape
+    if layer == "gcn":                       # gcn.py:29-37, graph_ops.adj_norm
+        an = torch.diag_embed(adj.sum(-1) ** -1.0) @ adj
+        return torch.tanh((an @ x) @ t[pre + "gcn/linear/kernel"])
+    if layer == "gat1":
+        adj = torch.clamp(adj + torch.eye(n, dtype=adj.dtype)[None], max=1.0)
+    ei = torch.nonzero(adj != 0)             # tf.where order: (batch, sender, receiver)
+    b, snd, rcv = ei[:, 0], ei[:, 1], ei[:, 2]
+    seg = rcv + b * n
+
+    def seg_sum(v):
+        out = torch.zeros((B * n,) + v.shape[1:], dtype=v.dtype)
+        return out.index_add(0, seg, v)
+
+    cnt = seg_sum(torch.ones(len(seg), dtype=x.dtype))
+    if layer == "mpnn":                      # gcn.py:57-94
+        msgs = seg_sum(x[b, snd] @ t[pre + "mpnn/msg/kernel"]) / torch.clamp(cnt, min=1)[:, None]
+        return torch.tanh(x @ t[pre + "mpnn/node/kernel"] + msgs.reshape(B, n, H))
+    if layer == "mpnn2":                     # gcn.py:113-150
+        e = torch.cat([x[b, snd], x[b, rcv]], -1) @ t[pre + "mpnn2/msg/kernel"]
+        m = (seg_sum(e) / torch.clamp(cnt, min=1)[:, None]).reshape(B, n, H)
+        return torch.tanh(torch.cat([x, m], -1) @ t[pre + "mpnn2/node/kernel"])
+    # gat1: gcn.py:171-206, graph_ops.segment_softmax
+    z = x @ t[pre + "gat1/pre_att/kernel"]
+    att = torch.cat([z[b, snd], z[b, rcv]], -1) @ t[pre + "gat1/att/kernel"]
+    att = torch.nn.functional.leaky_relu(att, 0.2)
+    ex = torch.exp(att)
+    att = ex / seg_sum(ex)[seg]
+    A = torch.zeros((B, n, n), dtype=x.dtype).index_put((b, snd, rcv), att[:, 0])
+    return torch.tanh(A @ z)
+
+
+@pytest.mark.parametrize("layer", O.GNN_LAYERS)
+@pytest.mark.parametrize("graph", ["ring", "random"])
+def test_gnn_layer_gradients_match_autograd(layer, graph):
+    """f4: GraphNet with each message-passing layer of models/gcn.py (MPNN, GCN, MPNN2, GAT1):
+    the oracle's forward and manual backward against torch autograd of the reference's call(),
+    on the ring graph and on random directed graphs (every node with an in-edge)."""
+    rng = np.random.default_rng(11)
+    p = O.gnn_init(rng, 4, layer=layer)
+    p["actor/linear_out/kernel"] *= 30
+    p["critic/linear_out/kernel"] *= 30
+    n = 24
+    X = rng.normal(size=(n, 4, 23)).astype(np.float32)
+    node = rng.integers(0, 4, size=n)
+    if graph == "ring":
+        adj = np.broadcast_to(O.ring_adjacency(), (n, 4, 4)).astype(np.float32)
+    else:
+        adj = (rng.random((n, 4, 4)) < 0.5).astype(np.float32)
+        adj[:, np.arange(4), (np.arange(4) + 1) % 4] = 1.0    # every row and column non-empty
+    b = _rand_batch(rng, n, 0, 2, X=True)
+    logits, value, cache = O.gnn_forward(p, X, node, adj, layer=layer)
+    dl, dv, st = O.ppo_loss_rows(logits, value, b["actions"], b["logits"], b["logp"],
+                                 b["vf_preds"], b["adv"], b["vt"], np.float32(0.2))
+    g = O.gnn_backward(p, cache, dl, dv)
+    assert sorted(g) == sorted(p)
+
+    t = {k: torch.tensor(v, dtype=torch.float64, requires_grad=True) for k, v in p.items()}
+    adj_t = torch.tensor(adj, dtype=torch.float64)
+    Xt = torch.tensor(X, dtype=torch.float64)
+
+    def net(pre):
+        f, q = Xt[..., :19], Xt[..., 19:]
+        wn = torch.tanh(q @ t[pre + "state_enc/kernel"] + t[pre + "state_enc/bias"]).reshape(n, 4, 19, 64)
+        h = torch.tanh(torch.einsum("bni,bnij->bnj", f, wn))
+        y = _torch_gnn_layer(layer, t, pre, h, adj_t)
+        return y[torch.arange(n), torch.tensor(node)] @ t[pre + "linear_out/kernel"] + t[pre + "linear_out/bias"]
+
+    la, lv = net("actor/"), net("critic/")
+    np.testing.assert_allclose(logits, la.detach().numpy(), rtol=1e-4, atol=1e-5)
+    loss = _torch_ppo_loss(la, lv[:, 0], b, 0.2, {})
+    loss.backward()
+    assert abs(loss.item() - st["total_loss"]) < 1e-5 * max(1, abs(loss.item()))
+    for k in p:
+        ref = t[k].grad.numpy()
+        assert np.abs(ref).max() > 0, k
+        np.testing.assert_allclose(g[k], ref, rtol=1e-4, atol=2e-5 * np.abs(ref).max(), err_msg=k)
+
+
 def test_gae_matches_direct_recursion():
     rng = np.random.default_rng(1)
     T, C = 50, 7
