@@ -40,7 +40,7 @@ int fail(const std::string& msg) {
   if (!(c)) return fail("null context")
 
 int ffn_param_count(int d, int A) { return d * 64 * 2 + 128 + 2 * 4096 + 128 + 64 * 2 * A + 2 * A + 65; }
-int gnn_param_count(int A) { return gnn_param_total(A); }
+int gnn_param_count(int A, int layer) { return gnn_param_total(A, layer); }
 
 struct Policy {
   int k = 0, d = 0, C = 0, n_params = 0, R = 0, nb = 0;
@@ -130,6 +130,7 @@ static int validate(const ddrl_cfg& c) {
   if (c.model_kind == DDRL_MODEL_GNN && (c.n_policies != 1 || c.n_agents != 4 || c.obs_dim[0] != 19))
     return fail("gnn requires one shared leg policy, 4 agents and 19 features per node");
   if (c.model_kind == DDRL_MODEL_GNN && c.act_dim != 2) return fail("gnn kernels are built for act_dim 2");
+  if (c.gnn_layer < DDRL_GNN_MPNN || c.gnn_layer > DDRL_GNN_GAT1) return fail("gnn_layer must be one of DDRL_GNN_*");
   if (c.leg_coupling && (c.model_kind != DDRL_MODEL_FFN || c.act_dim != 2 || c.n_policies != 1 || c.n_agents != 4 ||
                           c.obs_dim[0] > 20))
     return fail("leg_coupling (\"cup\") requires the fcnet model, one shared leg policy, 4 agents, act_dim 2 and obs_dim <= 20");
@@ -186,7 +187,7 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
     P.R = T * P.C;
     P.nb = std::max(1, P.R / g.sgd_minibatch_size);
     P.lay = make_layout(g, P.d);
-    P.n_params = g.model_kind == DDRL_MODEL_FFN ? ffn_param_count(P.d, g.act_dim) : gnn_param_count(g.act_dim);
+    P.n_params = g.model_kind == DDRL_MODEL_FFN ? ffn_param_count(P.d, g.act_dim) : gnn_param_count(g.act_dim, g.gnn_layer);
     if (g.leg_coupling) P.n_params += 4 * g.act_dim;   // leg_coupling [4][A] after the fcnet variables
     PolicyRoute& pr = ra.pol[p];
     pr.k = P.k; pr.d = P.d;
@@ -229,8 +230,11 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
     c->gnn.part_stride = (np + 3) & ~3;   // 16-byte aligned tile rows (float4 partial stores)
     c->gnn.grad = c->pol[0].grad;
     rc = dalloc(c, &c->gnn.part, (size_t)(DDRL_MB / 4) * c->gnn.part_stride) || dalloc(c, &c->gnn.statp, 2 * (DDRL_MB / 4) * 8) ||
-         dalloc(c, &c->gnn.normp, (np + 255) / 256) || dalloc(c, &c->gnn.bp_cur, 2) ||
-         dalloc(c, &c->gnn.chunk, (size_t)GNN_CHUNK_STEPS * DDRL_MB * c->pol[0].lay.stride);
+         dalloc(c, &c->gnn.normp, (np + 255) / 256) || dalloc(c, &c->gnn.bp_cur, 2);
+    // the record chunk of the fused update is allocated by the first ddrl_ppo_update (forward-only
+    // and data-parallel contexts never need it), sized to the schedule when that is shorter
+    c->gnn.chunk = nullptr;
+    c->gnn.chunk_steps = std::min(GNN_CHUNK_STEPS, g.num_sgd_iter * c->pol[0].nb);
   }
   if (!rc) {
     float* tab[DDRL_MAXP] = {nullptr};
@@ -478,7 +482,7 @@ static ActArgs make_act(ddrl_ctx* c, int t, const float* eps, float* actions, in
 
 static int launch_act(ddrl_ctx* c, const ActArgs& aa) {
   if (c->cfg.model_kind == DDRL_MODEL_FFN) launch_act_ffn(c->stream, c->route, aa);
-  else launch_act_gnn(c->stream, c->route, aa);
+  else launch_act_gnn(c->stream, c->route, aa, c->cfg.gnn_layer);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -728,15 +732,18 @@ int ddrl_ppo_update(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const 
                       c->cfg.leg_coupling, c->xchg, c->gx, c->update_split, c->err, &c->upd_epoch);
   else if (c->pol[0].last_steps > 0) {   // one shared policy
     const int last = c->pol[0].last_steps;
+    if (!c->gnn.chunk && dalloc(c, &c->gnn.chunk, (size_t)c->gnn.chunk_steps * DDRL_MB * c->pol[0].lay.stride))
+      return -1;
+    const int CH = c->gnn.chunk_steps;
     // the records of each run of GNN_CHUNK_STEPS steps are gathered into one contiguous
     // chunk first (stream order: after the previous run's last step), so every gradient
     // launch reads its minibatch without dependent index loads
     const size_t step_floats = (size_t)DDRL_MB * ua[0].lay.stride;
     for (int step = 0; step < last; ++step) {
-      const int k = step % GNN_CHUNK_STEPS;
-      if (k == 0) launch_gnn_gather(c->stream, ua[0], step, std::min(GNN_CHUNK_STEPS, last - step), c->gnn.chunk);
+      const int k = step % CH;
+      if (k == 0) launch_gnn_gather(c->stream, ua[0], step, std::min(CH, last - step), c->gnn.chunk);
       launch_step_gnn(c->stream, ua[0], h, step, 128, 1.f / c->cfg.sgd_minibatch_size, c->gnn,
-                      c->gnn.chunk + k * step_floats);
+                      c->gnn.chunk + k * step_floats, c->cfg.gnn_layer);
     }
   }
   HIPCHK(hipGetLastError());
@@ -784,7 +791,7 @@ int ddrl_ppo_grad(ddrl_ctx* c, int pid, const int32_t* rows, int n_rows, float k
                       c->pol[pid].d, c->pol[pid].lay.stride, c->cfg.leg_coupling, c->xchg, c->gx,
                       grad_split(c, n_rows), c->err, &c->upd_epoch);
   else
-    launch_step_gnn(c->stream, u, h, 0, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->gnn);
+    launch_step_gnn(c->stream, u, h, 0, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->gnn, nullptr, c->cfg.gnn_layer);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -857,7 +864,7 @@ int ddrl_ppo_update_ddp(ddrl_ctx* c, int pid, const int32_t* shuffle, const int3
       launch_update_ffn(c->stream, &ua[s], h, m, inv_n, c->cfg.act_dim, P.d, P.lay.stride, c->cfg.leg_coupling,
                         c->xchg, c->gx, grad_split(c, m), c->err, &c->upd_epoch);
     else
-      launch_step_gnn(c->stream, ua[s], h, 0, m, inv_n, c->gnn);
+      launch_step_gnn(c->stream, ua[s], h, 0, m, inv_n, c->gnn, nullptr, c->cfg.gnn_layer);
     NCCLCHK(ncclAllReduce(P.grad, P.grad, (size_t)P.n_params, ncclFloat32, ncclSum, c->comm, c->stream));
     launch_apply_adam(c->stream, P.grad, P.n_params, P.theta, P.m, P.v, P.beta_pow, h, gscale, pid);
   }
@@ -883,7 +890,7 @@ int ddrl_policy_forward(ddrl_ctx* c, int pid, const float* obs, const int32_t* n
   fa.logits = logits; fa.values = values;
   fa.cup = c->cfg.leg_coupling ? P.theta + ffn_param_count(P.d, c->cfg.act_dim) : nullptr;
   if (c->cfg.model_kind == DDRL_MODEL_FFN) launch_forward_ffn(c->stream, fa);
-  else launch_forward_gnn(c->stream, fa);
+  else launch_forward_gnn(c->stream, fa, c->cfg.gnn_layer);
   HIPCHK(hipGetLastError());
   return 0;
 }

@@ -25,12 +25,23 @@
 //   backward : the reverse of the above; weight gradients of Wmsg / Wnode as 16x16 tiles
 //              over the 16 rows (MFMA, LDS images), Wenc / benc / Wout gradients by DPP
 //              transpose-reductions over the 16 rows of a DPP row.
+// Message-passing layer (template L, model_config "gnn_layer"; models/graph_net.py:20 selects
+// one of models/gcn.py's layers, MPNN by default), on the ring where every node has the two
+// neighbours n - 1, n + 1 (ring(x)_n = (x_{n-1} + x_{n+1}) / 2, DPP quad moves):
+//   MPNN  (gcn.py:57-94)    y = tanh(h Wnode + ring(h Wmsg))
+//   GCN   (gcn.py:29-37)    y = tanh(ring(h) W)          (graph_ops.adj_norm: D^-1 A)
+//   MPNN2 (gcn.py:113-150)  m = ring(h Wmsg[:64]) + h Wmsg[64:],  y = tanh(h Wnode[:64] + m Wnode[64:])
+//   GAT1  (gcn.py:171-206)  z = h Wp, e_sr = leaky_relu(z_s a[:64] + z_r a[64:]) over the ring with
+//                           self loops, alpha_sr = exp(e_sr) / sum_s' exp(e_s'r) (softmax over the
+//                           senders of r, graph_ops.segment_softmax), y_s = tanh(sum_r alpha_sr z_r)
+//                           (the reference's attention @ x aggregates along the sender row)
 // Training steps are three launches: per-tile partial gradients (k_gnn<MODE_GRAD>), a
 // fixed-order reduction over tiles + squared norm partials (k_gnn_reduce), and
 // clip_by_global_norm + tf1 Adam (k_gnn_adam).  A DDP step stops after the reduction.
 #include "common.h"
 #include "kernels.h"
 #include "ppo_loss.h"
+#include "ddrl_hip.h"   // DDRL_GNN_* layer ids
 
 #define GF 19              // leg features per node
 #define GHE (GF * 64)      // hypernetwork output width (1216)
@@ -64,16 +75,27 @@ __device__ __forceinline__ int gnn_hbwd_owner(int k, int t) {
   return (GNN_Z == 4 && k == GNI - 1) ? t : k % GNN_Z;
 }
 
+// Layer kernels of a net, in the reference's variable order: "wmsg" holds MPNN msg_transform,
+// GCN linear, MPNN2 msg_transform [128][64] or GAT1 pre_att_linear; "wnode" holds MPNN
+// node_update, MPNN2 node_update [128][64] or GAT1 att_linear [128][1] (GCN: none).
+__host__ __device__ constexpr int gnn_msg_floats(int L) { return L == DDRL_GNN_MPNN2 ? 8192 : 4096; }
+__host__ __device__ constexpr int gnn_node_floats(int L) {
+  return L == DDRL_GNN_MPNN ? 4096 : (L == DDRL_GNN_MPNN2 ? 8192 : (L == DDRL_GNN_GAT1 ? 128 : 0));
+}
+// 16 x 16 weight-gradient tiles of the layer per net (16 per 64 x 64 matrix)
+__host__ __device__ constexpr int gnn_layer_mats(int L) {
+  return L == DDRL_GNN_MPNN ? 2 : (L == DDRL_GNN_MPNN2 ? 4 : 1);
+}
 struct GnnNetOff { int wenc, benc, wmsg, wnode, wout, bout; };
-__host__ __device__ inline GnnNetOff gnn_net_off(int A, int net) {
-  const int actor = 4 * GHE + GHE + 2 * 4096 + 64 * 2 * A + 2 * A;
+__host__ __device__ inline GnnNetOff gnn_net_off(int A, int net, int L = DDRL_GNN_MPNN) {
+  const int actor = 4 * GHE + GHE + gnn_msg_floats(L) + gnn_node_floats(L) + 64 * 2 * A + 2 * A;
   const int O = net ? 1 : 2 * A;
   GnnNetOff o;
   o.wenc = net ? actor : 0;
   o.benc = o.wenc + 4 * GHE;
   o.wmsg = o.benc + GHE;
-  o.wnode = o.wmsg + 4096;
-  o.wout = o.wnode + 4096;
+  o.wnode = o.wmsg + gnn_msg_floats(L);
+  o.wout = o.wnode + gnn_node_floats(L);
   o.bout = o.wout + 64 * O;
   return o;
 }
@@ -95,6 +117,10 @@ __device__ __forceinline__ float quad_next(float v) { return dpp_mov<0x39>(v); }
 #define L_TP (L_SEL + 8)          // per-wave 2 x 4 x 16x16 transpose tiles of the hypernet backward
 #define L_QT (L_TP + 8 * 1024)    // quaternions of the tile's 16 graph-nodes [16][4]
 #define L_TOTAL (L_QT + 64)
+// inside L_TP (used only by the hypernetwork backward, after every layer tile is done):
+#define L_M (L_TP)                // MPNN2: message image m [16][64] swizzled
+#define L_DMR (L_TP + 1024)       // MPNN2: ring(dm) image
+#define L_GA (L_TP + 2048)        // GAT1: cross-wave partial dots [4 waves][16 nodes][4]
 
 // Partial-gradient stores: read once, by the reduction kernel, mostly on other XCDs.
 // Nontemporal stores stream them out of the XCD's L2 while the kernel runs instead of
@@ -104,7 +130,9 @@ __device__ __forceinline__ void pst(float* p, float v) { __builtin_nontemporal_s
 __device__ __forceinline__ void pst4(float* p, floatx4 v) {
   __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(p));
 }
-template <int A, int MODE, int NET>
+__device__ __forceinline__ float leaky02(float x) { return x > 0.f ? x : 0.2f * x; }   // tf.nn.leaky_relu
+
+template <int A, int MODE, int NET, int L>
 __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
   constexpr int O = NET ? 1 : 2 * A;
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, q = lane >> 4, w = tid >> 6;
@@ -112,7 +140,7 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
   const int g = c >> 2, n = c & 3;
   const int graph = 4 * tile + g;
   const bool gvalid = graph < ga.n_graphs;
-  const GnnNetOff off = gnn_net_off(A, NET);
+  const GnnNetOff off = gnn_net_off(A, NET, L);
   const float* __restrict__ th = ga.theta;
   if (MODE == GNN_ACT && NET == 0 && ga.bootstrap) return;   // bootstrap: critic only
 #ifdef DDRL_ABL_GNN_EMPTY
@@ -161,15 +189,31 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
       be[k][t] = i < GF ? *reinterpret_cast<const floatx4*>(th + off.benc + j + 4 * q) : splat4(0.f);
     }
   }
-  float wmf[4][4], wnf[4][4], wo[4][O];
+  // layer weights of output block w (A operand: W[k = 16 fb + 4 q + r][16 w + c]):
+  //   wmf: MPNN msg / GCN linear / MPNN2 msg rows 0-63 / GAT1 pre_att;  wnf: MPNN node / MPNN2
+  //   node rows 0-63;  wm2 / wn2: MPNN2 msg / node rows 64-127
+  constexpr bool TWO = L == DDRL_GNN_MPNN || L == DDRL_GNN_MPNN2;
+  constexpr bool M2 = L == DDRL_GNN_MPNN2;
+  float wmf[4][4], wnf[TWO ? 4 : 1][4], wm2[M2 ? 4 : 1][4], wn2[M2 ? 4 : 1][4], wo[4][O];
 #pragma unroll
   for (int fb = 0; fb < 4; ++fb)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int k = 16 * fb + 4 * q + r;
       wmf[fb][r] = th[off.wmsg + k * 64 + 16 * w + c];
-      wnf[fb][r] = th[off.wnode + k * 64 + 16 * w + c];
+      if constexpr (TWO) wnf[fb][r] = th[off.wnode + k * 64 + 16 * w + c];
+      if constexpr (M2) {
+        wm2[fb][r] = th[off.wmsg + (64 + k) * 64 + 16 * w + c];
+        wn2[fb][r] = th[off.wnode + (64 + k) * 64 + 16 * w + c];
+      }
     }
+  // GAT1 attention vector at this lane's output features 16 w + 4 q + r (sender / receiver half)
+  float at1[4], at2[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    at1[r] = L == DDRL_GNN_GAT1 ? th[off.wnode + 16 * w + 4 * q + r] : 0.f;
+    at2[r] = L == DDRL_GNN_GAT1 ? th[off.wnode + 64 + 16 * w + 4 * q + r] : 0.f;
+  }
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -214,20 +258,78 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) h[fb][r] = himg[wbase(r) + 16 * fb];
 
-  // ---- MPNN: msg and node for output block w ----
-  floatx4 msg = splat4(0.f), nod = splat4(0.f);
+  // ---- message-passing layer: output block w of y (lane: node c, features 16 w + 4 q + r) ----
+  float y[4];
+  float* mimg = lds + L_M;
+  float* ga_s = lds + L_GA;
+  // GAT1 state kept for the backward: z (block w), attention of this node as sender to its
+  // prev / self / next receivers, the per-node score halves and softmax denominators
+  floatx4 zf = splat4(0.f);
+  float gp = 0.f, gu = 0.f, aSp = 0.f, aSs = 0.f, aSn = 0.f;
+  if constexpr (L == DDRL_GNN_MPNN) {
+    floatx4 msg = splat4(0.f), nod = splat4(0.f);
 #pragma unroll
-  for (int fb = 0; fb < 4; ++fb)
+    for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        msg = mfma4(wmf[fb][r], h[fb][r], msg);
+        nod = mfma4(wnf[fb][r], h[fb][r], nod);
+      }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      msg = mfma4(wmf[fb][r], h[fb][r], msg);
-      nod = mfma4(wnf[fb][r], h[fb][r], nod);
+      const float m = 0.5f * (quad_next(msg[r]) + quad_prev(msg[r]));
+      y[r] = tanh_fast(nod[r] + m);
     }
-  float y[4];
+  } else if constexpr (L == DDRL_GNN_GCN) {
+    floatx4 msg = splat4(0.f);
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float m = 0.5f * (quad_next(msg[r]) + quad_prev(msg[r]));
-    y[r] = tanh_fast(nod[r] + m);
+    for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) msg = mfma4(wmf[fb][r], h[fb][r], msg);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y[r] = tanh_fast(0.5f * (quad_next(msg[r]) + quad_prev(msg[r])));
+  } else if constexpr (L == DDRL_GNN_MPNN2) {
+    floatx4 ma = splat4(0.f), mb = splat4(0.f), nod = splat4(0.f);
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        ma = mfma4(wmf[fb][r], h[fb][r], ma);
+        mb = mfma4(wm2[fb][r], h[fb][r], mb);
+        nod = mfma4(wnf[fb][r], h[fb][r], nod);
+      }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) mimg[wbase(r) + 16 * w] = 0.5f * (quad_next(ma[r]) + quad_prev(ma[r])) + mb[r];
+    __syncthreads();
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) nod = mfma4(wn2[fb][r], mimg[wbase(r) + 16 * fb], nod);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y[r] = tanh_fast(nod[r]);
+  } else {   // GAT1
+#pragma unroll
+    for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) zf = mfma4(wmf[fb][r], h[fb][r], zf);
+    float pp = 0.f, uu = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { pp = fmaf(zf[r], at1[r], pp); uu = fmaf(zf[r], at2[r], uu); }
+    pp = qsum(pp);
+    uu = qsum(uu);
+    if (q == 0) { ga_s[(w * 16 + c) * 4] = pp; ga_s[(w * 16 + c) * 4 + 1] = uu; }
+    __syncthreads();
+    gp = ((ga_s[c * 4] + ga_s[(16 + c) * 4]) + ga_s[(32 + c) * 4]) + ga_s[(48 + c) * 4];
+    gu = ((ga_s[c * 4 + 1] + ga_s[(16 + c) * 4 + 1]) + ga_s[(32 + c) * 4 + 1]) + ga_s[(48 + c) * 4 + 1];
+    const float up = quad_prev(gu), un = quad_next(gu), pp_ = quad_prev(gp), pn = quad_next(gp);
+    // denominator of this node as receiver: its senders n - 1, n, n + 1
+    const float S = (__expf(leaky02(pp_ + gu)) + __expf(leaky02(gp + gu))) + __expf(leaky02(pn + gu));
+    aSp = __expf(leaky02(gp + up)) / quad_prev(S);
+    aSs = __expf(leaky02(gp + gu)) / S;
+    aSn = __expf(leaky02(gp + un)) / quad_next(S);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      y[r] = tanh_fast(aSp * quad_prev(zf[r]) + aSs * zf[r] + aSn * quad_next(zf[r]));
   }
   // ---- head: partial dot over this wave's 16 features, then across waves ----
   float* hp = lds + L_HP;
@@ -373,8 +475,8 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
     for (int gg = 0; gg < 4; ++gg) s += dsh[gg * 4 + tid] * (4 * tile + gg < ga.n_graphs ? 1.f : 0.f);
     pst(P + off.bout + tid, s);
   }
-  // dy -> du = dy (1 - y^2) -> dm (ring mean transposed)
-  float du[4], dm[4];
+  // dy -> du = dy (1 - y^2): gradient at the layer's pre-activation (lane: node c, block w)
+  float du[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     float dy = 0.f;
@@ -382,45 +484,148 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
     for (int o = 0; o < O; ++o) dy = fmaf(ds[o], wo[r][o], dy);
     du[r] = dy * (1.f - y[r] * y[r]);
   }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) dm[r] = 0.5f * (quad_next(du[r]) + quad_prev(du[r]));
   float* duimg = lds + L_DU;
   float* dmimg = lds + L_DM;
+  float* dmrimg = lds + L_DMR;
+  // A operands of the transposed products: W[16 w + c][16 fb + 4 q + r] of a [64 + 64][64] block
+  auto wt = [&](int base, int row0, float (*a)[4]) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    duimg[wbase(r) + 16 * w] = du[r];
-    dmimg[wbase(r) + 16 * w] = dm[r];
-  }
-  // weights for dh: A[c][q] = W[16 w + c][16 fb + 4 q + r]
-  float wnb[4][4], wmb[4][4];
+    for (int fb = 0; fb < 4; ++fb) {
+      const floatx4 v = *reinterpret_cast<const floatx4*>(th + base + (row0 + 16 * w + c) * 64 + 16 * fb + 4 * q);
 #pragma unroll
-  for (int fb = 0; fb < 4; ++fb) {
-    const floatx4 a = *reinterpret_cast<const floatx4*>(th + off.wnode + (16 * w + c) * 64 + 16 * fb + 4 * q);
-    const floatx4 b = *reinterpret_cast<const floatx4*>(th + off.wmsg + (16 * w + c) * 64 + 16 * fb + 4 * q);
+      for (int r = 0; r < 4; ++r) a[fb][r] = v[r];
+    }
+  };
+  // dh (block w) = sum over (W, image) of W . image^T
+  auto acc_t = [&](floatx4& acc, float (*a)[4], const float* img) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) { wnb[fb][r] = a[r]; wmb[fb][r] = b[r]; }
-  }
-  __syncthreads();
-  // dh (block w) = Wnode . du^T + Wmsg . dm^T ;  dz = dh (1 - h^2)
+    for (int fb = 0; fb < 4; ++fb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc = mfma4(a[fb][r], img[wbase(r) + 16 * fb], acc);
+  };
   floatx4 dh = splat4(0.f);
+  // weight-gradient tiles of the layer: (A image, B image, parameter base) per matrix
+  const float* tA[4];
+  const float* tB[4];
+  int tP[4];
+  if constexpr (L == DDRL_GNN_MPNN) {
+    float dm[4];
 #pragma unroll
-  for (int fb = 0; fb < 4; ++fb)
+    for (int r = 0; r < 4; ++r) dm[r] = 0.5f * (quad_next(du[r]) + quad_prev(du[r]));
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      dh = mfma4(wnb[fb][r], duimg[wbase(r) + 16 * fb], dh);
-      dh = mfma4(wmb[fb][r], dmimg[wbase(r) + 16 * fb], dh);
+      duimg[wbase(r) + 16 * w] = du[r];
+      dmimg[wbase(r) + 16 * w] = dm[r];
     }
+    float wnb[4][4], wmb[4][4];
+    wt(off.wnode, 0, wnb);
+    wt(off.wmsg, 0, wmb);
+    __syncthreads();
+    acc_t(dh, wnb, duimg);   // dh = Wnode . du^T + Wmsg . dm^T
+    acc_t(dh, wmb, dmimg);
+    tA[0] = himg; tB[0] = duimg; tP[0] = off.wnode;
+    tA[1] = himg; tB[1] = dmimg; tP[1] = off.wmsg;
+  } else if constexpr (L == DDRL_GNN_GCN) {
+    // dW = ring(h)^T du = h^T ring(du) (ring symmetric);  dh = W . ring(du)^T
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dmimg[wbase(r) + 16 * w] = 0.5f * (quad_next(du[r]) + quad_prev(du[r]));
+    float wmb[4][4];
+    wt(off.wmsg, 0, wmb);
+    __syncthreads();
+    acc_t(dh, wmb, dmimg);
+    tA[0] = himg; tB[0] = dmimg; tP[0] = off.wmsg;
+  } else if constexpr (L == DDRL_GNN_MPNN2) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) duimg[wbase(r) + 16 * w] = du[r];
+    float wa[4][4], wb2[4][4];
+    wt(off.wnode, 64, wb2);   // node_update rows 64-127 (the message half)
+    wt(off.wnode, 0, wa);     // node_update rows 0-63 (the node's own features)
+    __syncthreads();
+    floatx4 dm = splat4(0.f);
+    acc_t(dm, wb2, duimg);    // dm = Wnode[64:] . du^T
+    acc_t(dh, wa, duimg);     // dh = Wnode[:64] . du^T + ...
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      dmimg[wbase(r) + 16 * w] = dm[r];
+      dmrimg[wbase(r) + 16 * w] = 0.5f * (quad_next(dm[r]) + quad_prev(dm[r]));
+    }
+    wt(off.wmsg, 0, wa);      // msg_transform rows 0-63 (sender half)
+    wt(off.wmsg, 64, wb2);    // msg_transform rows 64-127 (receiver half)
+    __syncthreads();
+    acc_t(dh, wa, dmrimg);    // ... + Wmsg[:64] . ring(dm)^T + Wmsg[64:] . dm^T
+    acc_t(dh, wb2, dmimg);
+    tA[0] = himg; tB[0] = duimg; tP[0] = off.wnode;
+    tA[1] = mimg; tB[1] = duimg; tP[1] = off.wnode + 4096;
+    tA[2] = himg; tB[2] = dmrimg; tP[2] = off.wmsg;
+    tA[3] = himg; tB[3] = dmimg; tP[3] = off.wmsg + 4096;
+  } else {   // GAT1
+    // d alpha_sr = dv_s . z_r for r = prev / self / next (partial over this lane's 4 features)
+    float dap = 0.f, das = 0.f, dan = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      dap = fmaf(du[r], quad_prev(zf[r]), dap);
+      das = fmaf(du[r], zf[r], das);
+      dan = fmaf(du[r], quad_next(zf[r]), dan);
+    }
+    dap = qsum(dap); das = qsum(das); dan = qsum(dan);
+    if (q == 0) {
+      ga_s[(w * 16 + c) * 4] = dap;
+      ga_s[(w * 16 + c) * 4 + 1] = das;
+      ga_s[(w * 16 + c) * 4 + 2] = dan;
+    }
+    __syncthreads();
+    auto wsum = [&](int k) {
+      return ((ga_s[c * 4 + k] + ga_s[(16 + c) * 4 + k]) + ga_s[(32 + c) * 4 + k]) + ga_s[(48 + c) * 4 + k];
+    };
+    dap = wsum(0); das = wsum(1); dan = wsum(2);
+    // softmax over the senders of each receiver r: sum_s alpha_sr d alpha_sr, at lane r
+    const float col = (quad_prev(aSn * dan) + aSs * das) + quad_next(aSp * dap);
+    const float up = quad_prev(gu), un = quad_next(gu);
+    const float dp_ = aSp * (dap - quad_prev(col)) * (gp + up > 0.f ? 1.f : 0.2f);
+    const float ds_ = aSs * (das - col) * (gp + gu > 0.f ? 1.f : 0.2f);
+    const float dn_ = aSn * (dan - quad_next(col)) * (gp + un > 0.f ? 1.f : 0.2f);
+    const float dps = (dp_ + ds_) + dn_;                                   // d(z_s . a[:64])
+    const float dur = (quad_prev(dn_) + ds_) + quad_next(dp_);            // d(z_r . a[64:])
+    float dz[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      // attention-weighted part: z_r receives alpha_sr dv_s from its senders s = r - 1, r, r + 1
+      const float dzz = (quad_prev(aSn) * quad_prev(du[r]) + aSs * du[r]) + quad_next(aSp) * quad_next(du[r]);
+      dz[r] = dzz + dps * at1[r] + dur * at2[r];
+    }
+    // d a[:64] = sum over nodes of dps z, d a[64:] = sum of dur z (this tile's 16 nodes)
+    if (zs == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float a1 = row16_sum(dps * zf[r]);
+        const float a2 = row16_sum(dur * zf[r]);
+        if (c == 0) {
+          pst(P + off.wnode + 16 * w + 4 * q + r, a1);
+          pst(P + off.wnode + 64 + 16 * w + 4 * q + r, a2);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dmimg[wbase(r) + 16 * w] = dz[r];
+    float wpb[4][4];
+    wt(off.wmsg, 0, wpb);
+    __syncthreads();
+    acc_t(dh, wpb, dmimg);   // dh = Wp . dz^T
+    tA[0] = himg; tB[0] = dmimg; tP[0] = off.wmsg;
+  }
   // the hypernet partials are consumed: reuse PART for the dz exchange [block][r][lane]
 #pragma unroll
   for (int r = 0; r < 4; ++r) part[(4 * w + r) * 64 + lane] = dh[r] * (1.f - h[w][r] * h[w][r]);
-  // dWnode, dWmsg: 32 tiles of 16x16 over the 16 rows, 8 per wave (k % GNN_Z == zs here)
-#pragma unroll 2
-  for (int k = 0; k < 8; ++k) {
+  // layer weight gradients: 16 tiles of 16x16 per matrix over the 16 rows, 4 per wave and
+  // matrix; tile slot k of this wave belongs to this workgroup's share (gnn_tile_owner)
+  // (slot k of wave w: tile id w + 4 k -> matrix k / 4, row block k % 4, column block w)
+  constexpr int NKT = 4 * gnn_layer_mats(L);
+#pragma unroll
+  for (int k = 0; k < NKT; ++k) {
     if (gnn_tile_owner(k) != zs) continue;
-    const int id = w + 4 * k;            // 0..31
-    const int mat = id >> 4, kb = (id >> 2) & 3, ob = id & 3;
-    const floatx4 t = dw_tile<16>(himg, mat ? dmimg : duimg, kb, ob);
-    const int base = (mat ? off.wmsg : off.wnode) + 16 * ob + c;
+    const int mat = k >> 2, kb = k & 3, ob = w;
+    const floatx4 t = dw_tile<16>(tA[mat], tB[mat], kb, ob);
+    const int base = tP[mat] + 16 * ob + c;
 #pragma unroll
     for (int r = 0; r < 4; ++r) pst(P + base + (16 * kb + 4 * q + r) * 64, t[r]);
   }
@@ -527,12 +732,22 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
   }
 }
 
-template <int A, int MODE>
+template <int A, int MODE, int L>
 __global__ void __launch_bounds__(256) k_gnn(GnnArgs ga) {
   __shared__ float lds[L_TOTAL];
-  if (blockIdx.y == 0) gnn_tile<A, MODE, 0>(ga, lds);
-  else gnn_tile<A, MODE, 1>(ga, lds);
+  if (blockIdx.y == 0) gnn_tile<A, MODE, 0, L>(ga, lds);
+  else gnn_tile<A, MODE, 1, L>(ga, lds);
 }
+// k_gnn instance of a layer (MODE fixed)
+#define GNN_LAUNCH(MODE, L_, grid, s, ga)                                                            \
+  do {                                                                                              \
+    switch (L_) {                                                                                   \
+      case DDRL_GNN_GCN: hipLaunchKernelGGL((k_gnn<2, MODE, DDRL_GNN_GCN>), grid, dim3(256), 0, s, ga); break;     \
+      case DDRL_GNN_MPNN2: hipLaunchKernelGGL((k_gnn<2, MODE, DDRL_GNN_MPNN2>), grid, dim3(256), 0, s, ga); break; \
+      case DDRL_GNN_GAT1: hipLaunchKernelGGL((k_gnn<2, MODE, DDRL_GNN_GAT1>), grid, dim3(256), 0, s, ga); break;   \
+      default: hipLaunchKernelGGL((k_gnn<2, MODE, DDRL_GNN_MPNN>), grid, dim3(256), 0, s, ga); break;              \
+    }                                                                                               \
+  } while (0)
 
 // ---- reduction over tiles: grad[p] = sum_t part[t][p] (fixed order) + norm^2 partials ----
 // loss statistics of the step: statp [net][tile][8]; lane j < 10 sums (net, stat) j over the
@@ -652,7 +867,7 @@ void launch_gnn_gather(hipStream_t s, const UpdateArgs& u, int step0, int n_step
   hipLaunchKernelGGL(k_gnn_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, u, step0, n, dst);
 }
 
-int gnn_param_total(int A) { return gnn_net_off(A, 1).bout + 1; }
+int gnn_param_total(int A, int layer) { return gnn_net_off(A, 1, layer).bout + 1; }
 
 static void check_a(int A) {
   if (A != 2) {
@@ -661,7 +876,7 @@ static void check_a(int A) {
   }
 }
 
-void launch_act_gnn(hipStream_t s, const RouteArgs& ra, const ActArgs& aa) {
+void launch_act_gnn(hipStream_t s, const RouteArgs& ra, const ActArgs& aa, int layer) {
   check_a(ra.A);
   GnnArgs ga{};
   ga.theta = aa.theta[0];
@@ -673,19 +888,19 @@ void launch_act_gnn(hipStream_t s, const RouteArgs& ra, const ActArgs& aa) {
   ga.n_agents = ra.n_agents; ga.bootstrap = aa.bootstrap; ga.last_v = aa.last_v[0];
   for (int a = 0; a < 4; ++a)
     for (int j = 0; j < 8; ++j) ga.act_index[a][j] = ra.pol[0].act_index[a][j];
-  hipLaunchKernelGGL((k_gnn<2, GNN_ACT>), dim3((ga.n_graphs + 3) / 4, 2), dim3(256), 0, s, ga);
+  GNN_LAUNCH(GNN_ACT, layer, dim3((ga.n_graphs + 3) / 4, 2), s, ga);
 }
 
-void launch_forward_gnn(hipStream_t s, const ForwardArgs& fa) {
+void launch_forward_gnn(hipStream_t s, const ForwardArgs& fa, int layer) {
   check_a(fa.A);
   GnnArgs ga{};
   ga.theta = fa.theta; ga.n_graphs = fa.n; ga.x = fa.x; ga.node = fa.node;
   ga.logits = fa.logits; ga.values = fa.values;
-  hipLaunchKernelGGL((k_gnn<2, GNN_FWD>), dim3((fa.n + 3) / 4, 2), dim3(256), 0, s, ga);
+  GNN_LAUNCH(GNN_FWD, layer, dim3((fa.n + 3) / 4, 2), s, ga);
 }
 
 void launch_step_gnn(hipStream_t s, const UpdateArgs& u, const UpdateHyper& h, int step, int nrows, float inv_n,
-                     const GnnScratch& sc, const float* stage) {
+                     const GnnScratch& sc, const float* stage, int layer) {
   check_a(u.A);
   GnnArgs ga{};
   ga.theta = u.theta; ga.u = u; ga.h = h; ga.step = step; ga.n_graphs = nrows; ga.inv_n = inv_n;
@@ -693,9 +908,9 @@ void launch_step_gnn(hipStream_t s, const UpdateArgs& u, const UpdateHyper& h, i
   ga.bp_cur = sc.bp_cur; ga.grad = u.grad_out ? u.grad_out : sc.grad;
   ga.stage = stage;
   const int ntiles = (nrows + 3) / 4;
-  const int n = gnn_param_total(u.A);
+  const int n = gnn_param_total(u.A, layer);
   // tiles of the critic write their statistics after the actor's: statp [2][32][8]
-  hipLaunchKernelGGL((k_gnn<2, GNN_GRAD>), dim3(ntiles, 2, GNN_Z), dim3(256), 0, s, ga);
+  GNN_LAUNCH(GNN_GRAD, layer, dim3(ntiles, 2, GNN_Z), s, ga);
   const int nred = (n + 255) / 256;
 #ifdef DDRL_ABL_GNN_GRAD_ONLY   // ablation build (timing only): no reduction / Adam launches
   return;

@@ -77,7 +77,7 @@ struct ActArgs {
   int e0, e1;                      // env range of this call ([0, N) for a whole step)
 };
 void launch_act_ffn(hipStream_t s, const RouteArgs& ra, const ActArgs& aa);
-void launch_act_gnn(hipStream_t s, const RouteArgs& ra, const ActArgs& aa);
+void launch_act_gnn(hipStream_t s, const RouteArgs& ra, const ActArgs& aa, int layer);
 
 // ---- reward (a8) ----
 struct RewardArgs {
@@ -152,7 +152,7 @@ struct ForwardArgs {
   float* logits; float* values;
 };
 void launch_forward_ffn(hipStream_t s, const ForwardArgs& fa);
-void launch_forward_gnn(hipStream_t s, const ForwardArgs& fa);
+void launch_forward_gnn(hipStream_t s, const ForwardArgs& fa, int layer);
 
 // ---- GraphNet (gnn.hip): per-tile kernels, one minibatch step = grad / reduce / Adam ----
 struct GnnArgs {
@@ -179,14 +179,15 @@ struct GnnArgs {
 };
 struct GnnScratch {
   float* part; int part_stride; float* statp; float* normp; float* bp_cur; float* grad;
-  float* chunk;       // [GNN_CHUNK_STEPS][128][stride] records of a run of minibatch steps
+  float* chunk;       // [chunk_steps][128][stride] records of a run of minibatch steps
+  int chunk_steps;    // min(GNN_CHUNK_STEPS, the schedule's steps); chunk allocated on first use
 };
 #define GNN_CHUNK_STEPS 1024
-int gnn_param_total(int A);
+int gnn_param_total(int A, int layer);   // layer: DDRL_GNN_*
 // stage: the step's pre-gathered records (fused update) or null (data-parallel gradient of
 // explicit rows)
 void launch_step_gnn(hipStream_t s, const UpdateArgs& u, const UpdateHyper& h, int step, int nrows, float inv_n,
-                     const GnnScratch& sc, const float* stage = nullptr);
+                     const GnnScratch& sc, const float* stage, int layer);
 // the records of minibatch steps [step0, step0 + n_steps) of the schedule -> dst
 // ([n_steps][128][stride], n_steps <= GNN_CHUNK_STEPS): one bandwidth-bound gather per chunk
 void launch_gnn_gather(hipStream_t s, const UpdateArgs& u, int step0, int n_steps, float* dst);

@@ -204,7 +204,7 @@ struct RowData {
 template <int NW, int ROWS>
 __device__ __forceinline__ void issue_rows(const float* rec, int stride, int cpr, int cpr_l, const int* idxb,
                                            float* stg, int R, unsigned lds_bytes) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
   if (w == NW - 1) return;
   const int nchunk = ROWS * cpr_l;
   const float inv = 1.f / (float)cpr_l;
@@ -511,7 +511,9 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   float* stg = red + 256;                   // [ROWS][stride] records of the next step (16 B aligned)
   const int stride = U.lay.stride, cpr = stride >> 2, cpr_l = stg_chunks(stride, A);
 
-  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, q = lane >> 4, w = tid >> 6;
+  // w is wave-uniform: readfirstlane keeps it (and the tile indices derived from it) in SGPRs
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, q = lane >> 4,
+            w = __builtin_amdgcn_readfirstlane(tid >> 6);
   // Store cache policy of the exchange.  A run-time choice here cost 0.3 us per step (the
   // branches around every granule store, measured), so the device-coherent protocol is the
   // separate -DDDRL_XCHG_ATOMIC build and this one always stores plainly into the XCD's L2.

@@ -31,16 +31,26 @@ class ModelCatalog:
             raise KeyError(f"unknown custom_model {name!r}; registered: {sorted(_CATALOG)}") from None
 
 
-def glorot_gnn_flat(rng, A, hidden=64, feat=19):
-    """GraphNet init: state_enc / MPNN kernels Glorot(1.0), linear_out Glorot(0.01), biases 0."""
+def gnn_layer_kernel_shapes(layer, hidden=64):
+    """Kernels of the message-passing layer in Keras creation order (models/gcn.py: MPNN
+    msg_transform + node_update :46-47, GCN linear :19, MPNN2 msg_transform + node_update on
+    concatenations :102-103, GAT1 pre_att_linear + att_linear :159-160)."""
+    return {"mpnn": [(hidden, hidden), (hidden, hidden)], "gcn": [(hidden, hidden)],
+            "mpnn2": [(2 * hidden, hidden), (2 * hidden, hidden)],
+            "gat1": [(hidden, hidden), (2 * hidden, 1)]}[layer]
+
+
+def glorot_gnn_flat(rng, A, hidden=64, feat=19, layer="mpnn"):
+    """GraphNet init: state_enc / layer kernels Glorot(1.0) (GAT1's Keras default
+    glorot_uniform is the same law), linear_out Glorot(0.01), biases 0; actor then critic."""
     def g(fi, fo, s):
         lim = math.sqrt(6.0 * s / (fi + fo))
         return rng.uniform(-lim, lim, size=(fi, fo)).astype(np.float32)
     out = []
     for n_out in (2 * A, 1):
-        out += [g(4, feat * hidden, 1.0), np.zeros(feat * hidden, np.float32),
-                g(hidden, hidden, 1.0), g(hidden, hidden, 1.0),
-                g(hidden, n_out, 0.01), np.zeros(n_out, np.float32)]
+        out += [g(4, feat * hidden, 1.0), np.zeros(feat * hidden, np.float32)]
+        out += [g(fi, fo, 1.0) for fi, fo in gnn_layer_kernel_shapes(layer, hidden)]
+        out += [g(hidden, n_out, 0.01), np.zeros(n_out, np.float32)]
     return np.concatenate([o.reshape(-1) for o in out])
 
 

@@ -20,6 +20,8 @@ MAX_P, MAX_AG, MAX_OBS = 4, 4, 48
 MODEL_FFN, MODEL_GNN = 0, 1
 REWARD_PER_LEG, REWARD_GLOBAL, REWARD_NORM = 0, 1, 2
 VF_CLIP_RAY10, VF_CLIP_SQUARED = 0, 1
+# message-passing layer of the "gnn" model (models/graph_net.py:20 selects one of models/gcn.py's)
+GNN_LAYERS = {"mpnn": 0, "gcn": 1, "mpnn2": 2, "gat1": 3}
 
 i32, f32 = C.c_int32, C.c_float
 
@@ -39,7 +41,7 @@ class DdrlCfg(C.Structure):
         ("adam_beta1", f32), ("adam_beta2", f32), ("adam_eps", f32),
         ("vf_clip_mode", i32), ("sgd_minibatch_size", i32), ("num_sgd_iter", i32),
         ("act_negate", (i32 * 8) * MAX_AG), ("policy_filter", i32),
-        ("leg_coupling", i32),
+        ("leg_coupling", i32), ("gnn_layer", i32),
     ]
 
 
@@ -119,7 +121,7 @@ def header_symbols(path=HEADER):
     return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(ddrl_\w+)\s*\(", txt, re.M)))
 
 
-ABI_VERSION = 3   # DDRL_ABI_VERSION of include/ddrl_hip.h (ddrl_cfg layout, record layout)
+ABI_VERSION = 4   # DDRL_ABI_VERSION of include/ddrl_hip.h (ddrl_cfg layout, record layout)
 COMM_ID_BYTES = 128   # DDRL_COMM_ID_BYTES (sizeof ncclUniqueId)
 
 

@@ -540,17 +540,21 @@ def ffn_shapes(d, n_out, hidden=64):
             ("value_out/bias", (1,))]
 
 
-def gnn_shapes(n_out, hidden=64, feat=19):
+def gnn_shapes(n_out, hidden=64, feat=19, layer="mpnn"):
     """Variable order / shapes of the "gnn" model (models/shared_graphnet_glorot_uniform_init.py:
     32-33: actor GraphNet then critic GraphNet; models/graph_net.py:14-29 state_enc, MPNN
     msg_transform / node_update (models/gcn.py:46-47, no bias), linear_out).  No GNN checkpoint
     is published, so these names are not pinned by a reference file."""
+    names = {"mpnn": ["mpnn/msg_transform", "mpnn/node_update"], "gcn": ["gcn/linear"],
+             "mpnn2": ["mpnn2/msg_transform", "mpnn2/node_update"],
+             "gat1": ["gat1/pre_att_linear", "gat1/att_linear"]}[layer]
+    kshapes = {"mpnn": [(hidden, hidden)] * 2, "gcn": [(hidden, hidden)], "mpnn2": [(2 * hidden, hidden)] * 2,
+               "gat1": [(hidden, hidden), (2 * hidden, 1)]}[layer]
     out = []
     for net, no in (("actor", n_out), ("critic", 1)):
-        out += [(f"{net}/state_enc/kernel", (4, feat * hidden)), (f"{net}/state_enc/bias", (feat * hidden,)),
-                (f"{net}/mpnn/msg_transform/kernel", (hidden, hidden)),
-                (f"{net}/mpnn/node_update/kernel", (hidden, hidden)),
-                (f"{net}/linear_out/kernel", (hidden, no)), (f"{net}/linear_out/bias", (no,))]
+        out += [(f"{net}/state_enc/kernel", (4, feat * hidden)), (f"{net}/state_enc/bias", (feat * hidden,))]
+        out += [(f"{net}/{nm}/kernel", sh) for nm, sh in zip(names, kshapes)]
+        out += [(f"{net}/linear_out/kernel", (hidden, no)), (f"{net}/linear_out/bias", (no,))]
     return out
 
 

@@ -96,4 +96,13 @@ def make_cfg(env, n_envs, frag_len=None, config=None):
         raise ValueError(f"observation_filter {config['observation_filter']!r} is not supported")
     c.policy_filter = 1 if config["observation_filter"] == "MeanStdFilter" else 0
     c.leg_coupling = 1 if cup else 0
+    # "gnn_layer" (model_config; an extension): the message-passing layer the reference selects by
+    # editing models/graph_net.py:20 -- "mpnn" (its default), "gcn", "mpnn2" or "gat1"
+    layer = (config.get("model") or {}).get("custom_model_config", {}).get(
+        "gnn_layer", (config.get("model") or {}).get("gnn_layer", "mpnn"))
+    if layer not in N.GNN_LAYERS:
+        raise ValueError(f"gnn_layer {layer!r}: one of {sorted(N.GNN_LAYERS)}")
+    if layer != "mpnn" and inst.model_kind != "gnn":
+        raise ValueError(f"gnn_layer {layer!r} needs the graph env / 'gnn' model")
+    c.gnn_layer = N.GNN_LAYERS[layer]
     return c, inst

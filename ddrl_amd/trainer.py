@@ -90,7 +90,8 @@ class PPOTrainer:
                 self.ctx.params_set(p, theta)
             else:
                 from .models import glorot_gnn_flat
-                self.ctx.params_set(p, glorot_gnn_flat(self.rng, self.cfg.act_dim))
+                layer = {v: k for k, v in N.GNN_LAYERS.items()}[self.cfg.gnn_layer]
+                self.ctx.params_set(p, glorot_gnn_flat(self.rng, self.cfg.act_dim, layer=layer))
         self.kl_coeff = [float(c["kl_coeff"])] * P
         if env_backend is None:
             from .envs import SyntheticVecEnv
@@ -295,7 +296,7 @@ class PPOTrainer:
             if self.cfg.model_kind == N.MODEL_FFN:
                 shapes = ffn_shapes(d, 2 * A) + ([("leg_coupling", (4, A))] if self.cfg.leg_coupling else [])
             else:
-                shapes = gnn_shapes(2 * A)
+                shapes = gnn_shapes(2 * A, layer={v: k for k, v in N.GNN_LAYERS.items()}[self.cfg.gnn_layer])
             st = {"weights": self.ctx.params_get(p), "adam_m": m, "adam_v": v,
                   "beta_powers": (np.float32(b1), np.float32(b2)), "shapes": shapes, "obs_dim": d,
                   "filter": None, "filter_buffer": None}

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define DDRL_ABI_VERSION 3
+#define DDRL_ABI_VERSION 4
 #define DDRL_MAX_POLICIES 4
 #define DDRL_MAX_AGENTS 4
 #define DDRL_MAX_OBS 48
@@ -38,6 +38,10 @@ extern "C" {
 enum { DDRL_MODEL_FFN = 0, DDRL_MODEL_GNN = 1 };
 enum { DDRL_REWARD_PER_LEG = 0, DDRL_REWARD_GLOBAL = 1, DDRL_REWARD_NORM = 2 };
 enum { DDRL_VF_CLIP_RAY10 = 0, DDRL_VF_CLIP_SQUARED = 1 };
+/* message-passing layer of the "gnn" model (models/graph_net.py:20 selects one of
+ * models/gcn.py's layers: MPNN :39-94 (the reference's default), GCN :7-37, MPNN2 :96-150,
+ * GAT1 :153-206) */
+enum { DDRL_GNN_MPNN = 0, DDRL_GNN_GCN = 1, DDRL_GNN_MPNN2 = 2, DDRL_GNN_GAT1 = 3 };
 
 /* Static configuration of one context (one env shard of one trainer). */
 typedef struct ddrl_cfg {
@@ -80,6 +84,8 @@ typedef struct ddrl_cfg {
                                shared leg policy are scaled by a trainable table [4][A],
                                row = the agent's leg index (SharedDecentralLegID env, :66-114);
                                the table follows the fcnet variables in the parameter vector */
+  int32_t gnn_layer;        /* DDRL_GNN_* (model_kind GNN): the layer's kernels sit between the
+                               state encoder and linear_out of each net, in Keras order */
 } ddrl_cfg;
 
 typedef struct ddrl_ctx ddrl_ctx;

@@ -242,18 +242,20 @@ class CupOracleRollout(OracleRollout):
 GNN_ENV = "QuantrupedMultiEnv_DecentralShared_Graph"
 
 
-def init_gnn_params(ctx, seed, head_scale=1.0, A=2):
+def init_gnn_params(ctx, seed, head_scale=1.0, A=2, layer="mpnn"):
     rng = np.random.default_rng(seed)
-    p = O.gnn_init(rng, 2 * A)
+    p = O.gnn_init(rng, 2 * A, layer=layer)
     for net in ("actor/", "critic/"):
         p[net + "linear_out/kernel"] *= head_scale
         p[net + "state_enc/bias"] += (rng.normal(size=p[net + "state_enc/bias"].shape) * 0.2).astype(np.float32)
     p["actor/linear_out/bias"] += np.concatenate([np.zeros(A), -0.5 * np.ones(A)]).astype(np.float32)
-    ctx.params_set(0, O.pack(p, O.gnn_param_shapes(2 * A)))
+    ctx.params_set(0, O.pack(p, O.gnn_param_shapes(2 * A, layer=layer)))
     return p
 
 
 class GnnOracleRollout(OracleRollout):
+    layer = "mpnn"
+
     def __init__(self, cfg, inst, params, filt):
         super().__init__(cfg, inst, params[0] if isinstance(params, list) else params, filt)
         self.params = [params] if not isinstance(params, list) else params
@@ -272,7 +274,7 @@ class GnnOracleRollout(OracleRollout):
         N_ = X.shape[0]
         Xr = np.repeat(X, 4, axis=0)                     # row c = e * 4 + n
         node = np.tile(np.arange(4), N_)
-        logits, value, _ = O.gnn_forward(self.params[0], Xr, node)
+        logits, value, _ = O.gnn_forward(self.params[0], Xr, node, layer=self.layer)
         return Xr, node, logits, value
 
     def act(self, t, eps):
@@ -294,7 +296,7 @@ class GnnOracleRollout(OracleRollout):
         self.last_v = [self._forward_all()[3]]
 
 
-def drift_check(got, model, params, shapes, batch, sh, pe, kl, steps, factor=4.0, floor=2e-7):
+def drift_check(got, model, params, shapes, batch, sh, pe, kl, steps, factor=4.0, floor=2e-7, cfg=None):
     """Long-horizon parameter parity against the fp64 trajectory of the same algorithm.
 
     Runs the oracle's minibatch loop in fp32 (numpy) and in fp64 (oracle.with_dtype) over the
@@ -304,11 +306,10 @@ def drift_check(got, model, params, shapes, batch, sh, pe, kl, steps, factor=4.0
     Returns (e32, egpu, max |got - theta_fp32|, fp64 per-step stats, fp64 params)."""
     O64 = O.with_dtype(np.float64)
     n = sum(int(np.prod(s)) for _, s in shapes)
-    new32, _ = O.ppo_update(model, params, shapes, O.Adam(n), batch, sh, pe, np.float32(kl),
-                            {"entropy_coeff": 0.0}, steps=steps)
+    cfg = {"entropy_coeff": 0.0, **(cfg or {})}
+    new32, _ = O.ppo_update(model, params, shapes, O.Adam(n), batch, sh, pe, np.float32(kl), cfg, steps=steps)
     p64 = {k: np.asarray(v, np.float64) for k, v in params.items()}
-    new64, st64 = O64.ppo_update(model, p64, shapes, O64.Adam(n), batch, sh, pe, kl, {"entropy_coeff": 0.0},
-                                 steps=steps)
+    new64, st64 = O64.ppo_update(model, p64, shapes, O64.Adam(n), batch, sh, pe, kl, cfg, steps=steps)
     th32 = O.pack(new32, shapes).astype(np.float64)
     th64 = O64.pack(new64, shapes)
     got = np.asarray(got, np.float64)

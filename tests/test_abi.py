@@ -24,7 +24,7 @@ def test_exports_every_header_symbol(lib):
     for s in syms:
         assert hasattr(lib, s), s
     assert set(syms) == set(native._SIGS), set(syms) ^ set(native._SIGS)
-    assert lib.ddrl_abi_version() == native.ABI_VERSION == 3
+    assert lib.ddrl_abi_version() == native.ABI_VERSION == 4
 
 
 def test_cfg_struct_layout_matches_header():

@@ -46,10 +46,16 @@ def pg1():
                                          ("QuantrupedMultiEnv_SharedDecentral", 48, None),
                                          ("QuantrupedMultiEnv_DecentralShared_Graph", 24, None),
                                          ("QuantrupedMultiEnv_Centralized", 32, None),
-                                         ("QuantrupedMultiEnv_SharedDecentralLegID", 32, "cup")])
+                                         ("QuantrupedMultiEnv_SharedDecentralLegID", 32, "cup"),
+                                         ("QuantrupedMultiEnv_DecentralShared_Graph", 24, "gnn:gcn"),
+                                         ("QuantrupedMultiEnv_DecentralShared_Graph", 24, "gnn:mpnn2"),
+                                         ("QuantrupedMultiEnv_DecentralShared_Graph", 24, "gnn:gat1")])
 def test_trainer_iteration(env, n, model):
     from ddrl_amd.trainer import PPOTrainer
-    extra = {"model": {"custom_model": model}} if model else {}
+    extra = {}
+    if model:
+        name, _, layer = model.partition(":")
+        extra = {"model": {"custom_model": name, **({"gnn_layer": layer} if layer else {})}}
     tr = PPOTrainer({"env": env, "rollout_fragment_length": 8, **extra}, n_envs=n, seed=3)
     w0 = {k: v.copy() for k, v in tr.get_weights().items()}
     r = tr.train()

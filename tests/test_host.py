@@ -310,3 +310,26 @@ def test_host_dict_env_refuses_several_target_velocities():
         HostMultiAgentEnv("QuantrupedMultiEnv_Local", {"target_velocity": [0.5, 1.0]})
     env = HostMultiAgentEnv("QuantrupedMultiEnv_Local", {"target_velocity": [0.75, 0.75]})
     env.env.close()
+
+
+def test_gnn_layer_config_is_validated():
+    """f4: model_config "gnn_layer" selects the message-passing layer of the graph model
+    (models/graph_net.py:20 in the reference); unknown names and non-graph envs are refused."""
+    from ddrl_amd.spec import make_cfg
+    GNN_ENV = "QuantrupedMultiEnv_DecentralShared_Graph"
+    for name, code in N.GNN_LAYERS.items():
+        cfg, _ = make_cfg(GNN_ENV, 4, 2, {"model": {"custom_model": "gnn", "gnn_layer": name}})
+        assert cfg.gnn_layer == code
+    with pytest.raises(ValueError, match="gnn_layer"):
+        make_cfg(GNN_ENV, 4, 2, {"model": {"custom_model": "gnn", "gnn_layer": "sage"}})
+    with pytest.raises(ValueError, match="gnn_layer"):
+        make_cfg("QuantrupedMultiEnv_Local", 4, 2, {"model": {"gnn_layer": "gat1"}})
+
+
+@pytest.mark.parametrize("layer", ["mpnn", "gcn", "mpnn2", "gat1"])
+def test_glorot_gnn_init_matches_oracle_per_layer(layer):
+    from oracle import ddrl_oracle as O
+    from ddrl_amd.models import glorot_gnn_flat
+    shapes = O.gnn_param_shapes(4, layer=layer)
+    ref = O.pack(O.gnn_init(np.random.default_rng(6), 4, layer=layer), shapes)
+    np.testing.assert_array_equal(glorot_gnn_flat(np.random.default_rng(6), 2, layer=layer), ref)
