@@ -138,6 +138,96 @@ def cpu_baseline(env, n_envs=128, T=200, seed=0, threads=1):
                                 f"10 x {T * n_envs // 128} minibatches x {P} policies)"
 
 
+def _cpu_rollout_chunk(a):
+    """One rollout worker of the parallel CPU baseline: its own envs and its own env-side
+    MeanStdFilter (as every RLlib rollout worker process has), T steps, then GAE per policy."""
+    env, n_envs, T, seed = a
+    from threadpoolctl import threadpool_limits
+    from oracle import ddrl_oracle as O
+    from ddrl_amd.spec import make_cfg
+    with threadpool_limits(limits=1):
+        cfg, inst = make_cfg(env, n_envs, T)
+        rng = np.random.default_rng(seed)
+        P, A = cfg.n_policies, cfg.act_dim
+        agents = list(inst.agent_names)
+        params = [O.ffn_init(np.random.default_rng(1000 + p), cfg.obs_dim[p], 2 * A) for p in range(P)]
+        obs = rng.normal(size=(T + 1, n_envs, cfg.obs_full_dim)).astype(np.float32)
+        eps = rng.normal(size=(T, n_envs, cfg.n_agents, A)).astype(np.float32)
+        fw = rng.normal(size=(T, n_envs)).astype(np.float32)
+        cfrc = rng.normal(size=(T, n_envs, 14, 6)).astype(np.float32)
+        rs = O.RunningStat((cfg.obs_full_dim,))
+        rec = [dict(obs=[], act=[], logits=[], logp=[], vf=[]) for _ in range(P)]
+        rew = np.zeros((P, T, n_envs), np.float32)
+        tables = {a: inst.contact_force_indices[a] for a in agents}
+        z = O.mean_std_filter(obs[0], rs, True, 10.0)
+        for t in range(T):
+            actions = np.zeros((n_envs, 8))
+            for p in range(P):
+                x = z[:, inst.obs_indices[agents[p]]].astype(np.float32)
+                logits, value, _ = O.ffn_forward(params[p], x)
+                act = O.dg_sample(logits, eps[t, :, p])
+                for k, v in (("obs", x), ("act", act), ("logits", logits), ("logp", O.dg_logp(logits, act)),
+                             ("vf", value)):
+                    rec[p][k].append(v)
+                actions[:, inst.action_indices[agents[p]]] = np.clip(act, -1, 1)
+            for e in range(n_envs):
+                ad = {a: actions[e, inst.action_indices[a]] for a in agents}
+                rw = O.per_leg_reward(float(fw[t, e]), cfrc[t, e], ad, tables, 0.5, 0.05)
+                for p in range(P):
+                    rew[p, t, e] = rw[agents[p]]
+            z = O.mean_std_filter(obs[t + 1], rs, True, 10.0)
+        out = []
+        for p in range(P):
+            r = {k: np.stack(v) for k, v in rec[p].items()}
+            last_v = O.ffn_forward(params[p], z[:, inst.obs_indices[agents[p]]].astype(np.float32))[1]
+            adv, vt = O.gae_fragment(rew[p], r["vf"], np.zeros((T, n_envs), bool), last_v)
+            R = T * n_envs
+            out.append(dict(obs=r["obs"].reshape(R, -1), actions=r["act"].reshape(R, -1),
+                            logits=r["logits"].reshape(R, -1), logp=r["logp"].reshape(-1),
+                            vf_preds=r["vf"].reshape(-1), adv=adv.reshape(-1), vt=vt.reshape(-1)))
+    return out
+
+
+def _cpu_update_policy(a):
+    """One policy's minibatch SGD chain over the union batch (10 epochs; sequential by
+    construction: every step needs the previous step's weights)."""
+    env, p, batch, seed = a
+    from threadpoolctl import threadpool_limits
+    from oracle import ddrl_oracle as O
+    from ddrl_amd.spec import make_cfg
+    with threadpool_limits(limits=1):
+        cfg, _ = make_cfg(env, 1, 1)
+        A = cfg.act_dim
+        params = O.ffn_init(np.random.default_rng(1000 + p), cfg.obs_dim[p], 2 * A)
+        shapes = O.ffn_param_shapes(cfg.obs_dim[p], 2 * A)
+        adv, _, _ = O.standardize(batch["adv"])
+        sh, pe = O.sgd_schedule(np.random.default_rng(seed), len(adv), 128, 10)
+        adam = O.Adam(sum(int(np.prod(s)) for _, s in shapes))
+        O.ppo_update("ffn", params, shapes, adam, dict(batch, adv=adv), sh, pe, np.float32(0.2), {})
+    return p
+
+
+def cpu_baseline_parallel(env, n_envs=512, T=200, workers=16, seed=0):
+    """The iteration of cpu_baseline on `workers` host processes, parallel where the algorithm
+    is: the rollout over env chunks (one env-side filter per worker, like RLlib's rollout
+    workers), the PPO update over the independent policies (each policy's minibatch chain is
+    sequential; the 4 leg policies train side by side).  The pool is warmed before timing.
+    Run it in a process that has not initialised the GPU (bench.py starts a child for it)."""
+    import multiprocessing as mp
+    from ddrl_amd.spec import make_cfg
+    cfg, _ = make_cfg(env, n_envs, T)
+    P = cfg.n_policies
+    chunks = [c for c in (n_envs // workers + (1 if w < n_envs % workers else 0) for w in range(workers)) if c]
+    with mp.get_context("fork").Pool(len(chunks)) as pool:
+        pool.map(_cpu_rollout_chunk, [(env, 2, 2, 99)] * len(chunks))   # warm: imports in every worker
+        t0 = time.perf_counter()
+        parts = pool.map(_cpu_rollout_chunk, [(env, c, T, seed + 17 * w) for w, c in enumerate(chunks)])
+        batches = [{k: np.concatenate([pt[p][k] for pt in parts]) for k in parts[0][p]} for p in range(P)]
+        pool.map(_cpu_update_policy, [(env, p, batches[p], seed + 5 + p) for p in range(P)])
+        dt = time.perf_counter() - t0
+    return T * n_envs / dt, dt, len(chunks)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -152,6 +242,10 @@ def main():
     ap.add_argument("--ddp-mode", default="split", choices=["split", "local"],
                     help="shared-policy envs on N>1 GPUs: per-rank rows per SGD step (see ddrl_amd/ddp.py); "
                          "split (default) = the reference's 128-row minibatch SGD, local = 128 rows per rank")
+    ap.add_argument("--shared-mode", default="ddp", choices=["ddp", "gather"],
+                    help="N>1 GPUs: 'ddp' (shared-policy envs: RCCL all-reduce of the gradient every SGD step, "
+                         "the north-star mode) or 'gather' (any env: records all-gathered once per iteration, "
+                         "every rank runs the same fused update over the union batch; no per-step collective)")
     args = ap.parse_args()
 
     import torch
@@ -193,8 +287,11 @@ def main():
     gnn = cfg.model_kind == N.MODEL_GNN
     # shared-policy envs on several GPUs train data-parallel (identical weights on every
     # rank); independent-policy envs are replicas (own weights per rank)
-    ddp = (world > 1 or force_ddp) and P == 1
-    rng = np.random.default_rng(1234 if ddp else 1234 + rank)
+    ddp = (world > 1 or force_ddp) and P == 1 and args.shared_mode == "ddp"
+    gather = (world > 1 or force_ddp) and args.shared_mode == "gather"
+    if gather and args.envs % world:
+        raise SystemExit("--shared-mode gather needs --envs divisible by the number of ranks")
+    rng = np.random.default_rng(1234 if (ddp or gather) else 1234 + rank)
     from ddrl_amd.trainer import glorot_ffn_flat
     from ddrl_amd.models import glorot_gnn_flat
     for p in range(P):
@@ -205,7 +302,18 @@ def main():
     nb = [max(1, r // 128) for r in R]
     E = cfg.num_sgd_iter
     gen = torch.Generator(device=f"cuda:{local}")
-    gen.manual_seed(99 + rank)
+    gen.manual_seed(99 if gather else 99 + rank)   # gather: the same schedule on every rank
+    uctx = None
+    if gather:
+        # the learner context: the union batch of all ranks (rank-major), same weights everywhere
+        ucfg, _ = make_cfg(args.env, n_local * world, T)
+        uctx = N.Context(ucfg, local, stream.cuda_stream)
+        for p in range(P):
+            uctx.params_set(p, ctx.params_get(p))
+        R = [T * uctx.layout[p]["C"] for p in range(P)]
+        nb = [max(1, r // 128) for r in R]
+        from ddrl_amd.ddp import Comm, sync_standardize, standardize_constants
+        comm = Comm(f"cuda:{local}" if backend == "nccl" else "cpu") if dist is not None else None
     ev_upd = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     upd_ms = []
     if ddp:
@@ -260,6 +368,21 @@ def main():
                 upd_ms.append(ev_upd[0].elapsed_time(ev_upd[1]))
                 steps_done.append(pe.size)
             return
+        lctx = ctx
+        if gather:
+            lctx = uctx
+            for p in range(P):
+                sums = ctx.adv_sums_get(p)
+                uctx.adv_norm_set(p, *(sync_standardize(comm, sums) if comm else standardize_constants(sums)))
+                src, dst = ctx.records_tensor(p), uctx.records_tensor(p)
+                if comm is None:
+                    dst.copy_(src)
+                elif comm.device == "cpu":
+                    parts = [torch.empty_like(src, device="cpu") for _ in range(world)]
+                    dist.all_gather(parts, src.cpu())
+                    dst.copy_(torch.cat(parts).to(dst.device))
+                else:
+                    dist.all_gather_into_tensor(dst, src)
         # SampleBatch.shuffle + per-epoch minibatch permutations of every policy: one batched
         # argsort of fp64 uniforms each (policies of one env have equal batch sizes)
         if len(set(R)) == 1:
@@ -274,11 +397,14 @@ def main():
             perms = [torch.stack([torch.randperm(nb[p], device=stream.device, generator=gen, dtype=torch.int32)
                                   for _ in range(E)]).contiguous() for p in range(P)]
         ev_upd[0].record(stream)
-        ctx.ppo_update((1 << P) - 1, shuffles, perms, kl)
+        lctx.ppo_update((1 << P) - 1, shuffles, perms, kl)
         ev_upd[1].record(stream)
+        if gather:   # the next rollout uses the updated weights
+            for p in range(P):
+                ctx.params_set(p, uctx.params_get(p))
         # RLlib: update_kl with the last epoch's mean KL of every policy
         for p in range(P):
-            st = ctx.ppo_stats(p, E * nb[p])
+            st = lctx.ppo_stats(p, E * nb[p])
             mkl = float(np.mean(st[-nb[p]:, 3]))
             kl[p] = kl[p] * 1.5 if mkl > 2 * 0.01 else (kl[p] * 0.5 if mkl < 0.5 * 0.01 else kl[p])
         if record:
@@ -378,9 +504,13 @@ def main():
                if isinstance(learner, NativeDataParallelLearner) else
                f"{'RCCL' if backend == 'nccl' else backend} all-reduce of the gradient every SGD step, Python loop") \
         if ddp else ""
+    coll_name = "RCCL" if backend == "nccl" else backend
     parallelism = (f"data-parallel over {world} ranks: {ddp_how} "
                    f"({args.ddp_mode} mode, {rows_per_step} rows per rank per step)" if ddp else
-                   "replicas (no collective)")
+                   (f"gather over {world} ranks: every rank rolls out {n_local} envs, one {coll_name} all-gather "
+                    f"of the records per iteration, the same fused update over the union batch of "
+                    f"{n_local * world} envs on every rank (no per-step collective)" if gather else
+                    "replicas (no collective)"))
     result = {
         "metric": metric_name(args.envs),
         "value": env_steps / t_max,
@@ -421,14 +551,28 @@ def main():
         v, dt, sample = cpu_baseline(args.env, args.cpu_envs, T)
         result["cpu_baseline"] = {"value": v, "unit": "env-steps/s", "cores": 1, "kind": "port",
                                   "sample": sample + f"; {dt:.1f} s", "host_cpus": os.cpu_count()}
-        # the same sample with BLAS on this job's share of the host cores
-        # (OMP_NUM_THREADS on the GPU box; the machine's CPUs are shared between jobs)
+        # the same sample on this job's share of the host cores (OMP_NUM_THREADS
+        # on the GPU box; the machine's CPUs are shared between jobs), parallel over env chunks
+        # (rollout) and over the independent policies (update), in a child process that never
+        # touched the GPU (its worker pool forks)
         nthr = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count())
-        v2, dt2, _ = cpu_baseline(args.env, args.cpu_envs, T, threads=nthr)
-        result["cpu_baseline_all_cores"] = {"value": v2, "unit": "env-steps/s", "cores": nthr, "kind": "port",
-                                            "sample": f"same sample; {dt2:.1f} s"}
+        import subprocess
+        code = ("import json, bench; v, dt, w = bench.cpu_baseline_parallel(%r, %d, %d, %d); "
+                "print(json.dumps([v, dt, w]))" % (args.env, args.cpu_envs, T, nthr))
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600,
+                           cwd=os.path.dirname(os.path.abspath(__file__)))
+        if r.returncode == 0:
+            v2, dt2, w2 = json.loads(r.stdout.strip().splitlines()[-1])
+            result["cpu_baseline_all_cores"] = {
+                "value": v2, "unit": "env-steps/s", "cores": w2, "kind": "port",
+                "sample": f"same sample on {w2} worker processes: rollout over env chunks, update over the "
+                          f"{ctx.cfg.n_policies} policies; {dt2:.1f} s"}
+        else:
+            result["cpu_baseline_all_cores"] = {"error": r.stderr[-300:]}
     if rank == 0:
         print(json.dumps(result), flush=True)
+    if uctx is not None:
+        uctx.close()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

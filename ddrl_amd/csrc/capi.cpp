@@ -72,6 +72,18 @@ struct ddrl_ctx {
   unsigned upd_epoch = 0;              // update launches so far (granule tag epochs)
   int update_split = 2;                // workgroups per branch of the fused update (1 or 2)
   int* err = nullptr;                  // device error word (exchange timeout)
+  // Placement / rollback (fcnet update): the XCC of every block of the last update launch,
+  // the exchange protocol (0: plain stores into the XCD's L2, 1: relaxed agent-scope atomics,
+  // chosen by DDRL_XCHG=atomic or after a placement failure), and per policy a snapshot of
+  // theta | m | v | beta powers taken before each update, restored when the launch fails.
+  int* xcc = nullptr;
+  int xchg_atomic = 0;
+  int xcc_pending = 0;                 // blocks of an update launch not yet checked (grid size)
+  int xcc_ksp = 2;
+  int xcc_mask = 0;
+  int fail_step = -1;                  // test hook: DDRL_TEST_FAIL_STEP
+  float* snap[DDRL_MAXP] = {nullptr};
+  int snap_mask = 0;
   float kl_last[DDRL_MAXP] = {0};
   GnnScratch gnn{};               // GraphNet step scratch (per-tile partial gradients, ...)
   // host-variant staging
@@ -222,9 +234,14 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
        dalloc(c, &c->stage_tab, DDRL_MAXP) || dalloc(c, &c->zero_perm, 4) ||
        dalloc(c, &c->xchg, 8 * DDRL_MAXP) ||
        dalloc(c, &c->gx, gx_bytes(DDRL_MAXP) / sizeof(unsigned long long)) || dalloc(c, &c->err, 1) ||
+       dalloc(c, &c->xcc, 32) ||
        dalloc(c, &c->h_obs, (size_t)N * g.obs_full_dim) ||
        dalloc(c, &c->h_eps, (size_t)N * g.n_agents * g.act_dim) || dalloc(c, &c->h_act, (size_t)N * 8) ||
        dalloc(c, &c->h_fw, N) || dalloc(c, &c->h_cfrc, (size_t)N * 14 * 6) || dalloc(c, &c->h_done, N);
+  for (int p = 0; p < g.n_policies && !rc && g.model_kind == DDRL_MODEL_FFN; ++p)
+    rc = dalloc(c, &c->snap[p], 3 * (size_t)c->pol[p].n_params + 4);
+  if (const char* e = std::getenv("DDRL_XCHG")) c->xchg_atomic = std::string(e) == "atomic" ? 1 : 0;
+  if (const char* e = std::getenv("DDRL_TEST_FAIL_STEP")) c->fail_step = std::atoi(e);
   if (!rc && g.model_kind == DDRL_MODEL_GNN) {
     const int np = c->pol[0].n_params;
     c->gnn.part_stride = (np + 3) & ~3;   // 16-byte aligned tile rows (float4 partial stores)
@@ -266,17 +283,91 @@ int ddrl_set_stream(ddrl_ctx* c, void* s) {
   return 0;
 }
 
+// Snapshot of the policies an fcnet update launch is about to change (stream-ordered D2D copies:
+// theta | m | v | beta powers), restored by check_err when the launch fails.
+static int snapshot(ddrl_ctx* c, int mask) {
+  for (int p = 0; p < c->cfg.n_policies; ++p) {
+    if (!(mask & (1 << p)) || !c->snap[p]) continue;
+    Policy& P = c->pol[p];
+    const size_t n = (size_t)P.n_params;
+    HIPCHK(hipMemcpyAsync(c->snap[p], P.theta, n * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->snap[p] + n, P.m, n * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->snap[p] + 2 * n, P.v, n * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->snap[p] + 3 * n, P.beta_pow, 4 * 4, hipMemcpyDeviceToDevice, c->stream));
+  }
+  c->snap_mask = mask;
+  return 0;
+}
+
+static int restore_snapshot(ddrl_ctx* c) {
+  for (int p = 0; p < c->cfg.n_policies; ++p) {
+    if (!(c->snap_mask & (1 << p)) || !c->snap[p]) continue;
+    Policy& P = c->pol[p];
+    const size_t n = (size_t)P.n_params;
+    HIPCHK(hipMemcpyAsync(P.theta, c->snap[p], n * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(P.m, c->snap[p] + n, n * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(P.v, c->snap[p] + 2 * n, n * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(P.beta_pow, c->snap[p] + 3 * n, 4 * 4, hipMemcpyDeviceToDevice, c->stream));
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// The default exchange protocol needs the workgroups of one policy (blocks p, p + 8, ... of the
+// launch) on one XCD.  Returns 1 if the last launch's recorded XCC ids (HW_REG_XCC_ID) break that.
+static int placement_broken(ddrl_ctx* c) {
+  if (!c->xcc_pending) return 0;
+  int x[32] = {0};
+  if (hipMemcpy(x, c->xcc, sizeof(x), hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  const int per = 2 * c->xcc_ksp;   // workgroups per policy
+  int bad = 0;
+  for (int p = 0; p < 8; ++p) {
+    if (!(c->xcc_mask & (1 << p))) continue;
+    for (int j = 1; j < per && p + 8 * j < c->xcc_pending; ++j) bad |= x[p + 8 * j] != x[p];
+  }
+  c->xcc_pending = 0;
+  return bad;
+}
+
 static int check_err(ddrl_ctx* c) {
   int e = 0;
   HIPCHK(hipMemcpy(&e, c->err, sizeof(int), hipMemcpyDeviceToHost));
   if (e) {
     (void)hipMemset(c->err, 0, sizeof(int));
-    return fail("update kernel: an exchange between the workgroups of a policy timed out (3 s).  The "
-                "default protocol needs the workgroups of one policy on one XCD (round-robin dispatch); if "
-                "this machine places them otherwise, build the atomic-exchange library (`python -m "
-                "ddrl_amd.build --atomic`) and run with DDRL_LIB=libddrl_hip_atomic.so");
+    const int bad = placement_broken(c);
+    if (restore_snapshot(c)) return -1;
+    c->snap_mask = 0;
+    if (bad && !c->xchg_atomic) {
+      c->xchg_atomic = 1;
+      return fail("update kernel: the workgroups of a policy ran on different XCDs (placement check), so the "
+                  "default exchange through the XCD's L2 could not complete.  The weights, Adam state and beta "
+                  "powers are as before the call; this context has switched to the atomic exchange protocol "
+                  "(valid for any placement): call the update again");
+    }
+    return fail("update kernel: an exchange between the workgroups of a policy was abandoned (3 s timeout or "
+                "a failed launch).  The weights, Adam state and beta powers are as before the call");
   }
+  // a broken placement whose exchanges still completed (a granule reached the other XCD through
+  // memory) gave correct results -- the tags admit only this step's data -- but the next
+  // launch might not be so lucky: switch protocols now
+  if (placement_broken(c)) c->xchg_atomic = 1;
+  c->snap_mask = 0;
   return 0;
+}
+
+// fcnet update launch with the context's exchange protocol
+static void launch_ffn(ddrl_ctx* c, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n, int d,
+                       int stride, int ksp, int mask) {
+  c->xcc_pending = ksp == 2 ? 24 + h.P : 8 + h.P;
+  c->xcc_ksp = ksp;
+  c->xcc_mask = mask;
+  // test hook (DDRL_TEST_FAIL_STEP): a fused launch starts with the error word set, as an
+  // exchange abandoned in its first step would leave it -- every workgroup runs its steps and
+  // none writes back (no per-step cost in the kernel; a compare per step measured 0.18 us)
+  if (c->fail_step >= 0 && !ua->grad_out) (void)hipMemsetD32Async((hipDeviceptr_t)c->err, 1, 1, c->stream);
+  (c->xchg_atomic ? launch_update_ffn_atomic : launch_update_ffn)(
+      c->stream, ua, h, nrows, inv_n, c->cfg.act_dim, d, stride, c->cfg.leg_coupling, c->xchg, c->gx, ksp, c->err,
+      &c->upd_epoch, c->xcc);
 }
 
 int ddrl_synchronize(ddrl_ctx* c) {
@@ -727,9 +818,10 @@ int ddrl_ppo_update(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const 
   for (int i = 0; i < n; ++i) maxd = std::max(maxd, ua[i].d), maxs = std::max(maxs, ua[i].lay.stride);
   UpdateHyper h = make_hyper(c, n);
   // the arguments travel by value in the kernel's argument block (no copy from this stack frame)
-  if (c->cfg.model_kind == DDRL_MODEL_FFN)
-    launch_update_ffn(c->stream, ua, h, 128, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim, maxd, maxs,
-                      c->cfg.leg_coupling, c->xchg, c->gx, c->update_split, c->err, &c->upd_epoch);
+  if (c->cfg.model_kind == DDRL_MODEL_FFN) {
+    if (snapshot(c, mask & ((1 << c->cfg.n_policies) - 1))) return -1;
+    launch_ffn(c, ua, h, 128, 1.f / c->cfg.sgd_minibatch_size, maxd, maxs, c->update_split, (1 << n) - 1);
+  }
   else if (c->pol[0].last_steps > 0) {   // one shared policy
     const int last = c->pol[0].last_steps;
     if (!c->gnn.chunk && dalloc(c, &c->gnn.chunk, (size_t)c->gnn.chunk_steps * DDRL_MB * c->pol[0].lay.stride))
@@ -783,13 +875,13 @@ int ddrl_ppo_grad(ddrl_ctx* c, int pid, const int32_t* rows, int n_rows, float k
   if (stats_step >= c->cfg.num_sgd_iter * c->pol[pid].nb) return fail("stats_step beyond the stats buffer");
   UpdateArgs u = make_update(c, pid, rows, c->zero_perm, kl);
   u.nb = 1; u.n_epochs = 1; u.max_steps = 1; u.step0 = 0; u.grad_out = grad;
+  c->snap_mask = 0;   // a gradient launch changes no state: the caller's loop keeps its own snapshot
   u.stats = stats_step >= 0 ? c->pol[pid].stats + (size_t)stats_step * 8 : nullptr;
   c->kl_last[pid] = kl;
   UpdateHyper h = make_hyper(c, 1);
   if (c->cfg.model_kind == DDRL_MODEL_FFN)
-    launch_update_ffn(c->stream, &u, h, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim,
-                      c->pol[pid].d, c->pol[pid].lay.stride, c->cfg.leg_coupling, c->xchg, c->gx,
-                      grad_split(c, n_rows), c->err, &c->upd_epoch);
+    launch_ffn(c, &u, h, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->pol[pid].d, c->pol[pid].lay.stride,
+               grad_split(c, n_rows), 1);
   else
     launch_step_gnn(c->stream, u, h, 0, n_rows, 1.f / c->cfg.sgd_minibatch_size, c->gnn, nullptr, c->cfg.gnn_layer);
   HIPCHK(hipGetLastError());
@@ -801,7 +893,7 @@ int ddrl_ppo_apply(ddrl_ctx* c, int pid, const float* grad) {
   if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
   if (!grad) return fail("null grad");
   Policy& P = c->pol[pid];
-  launch_apply_adam(c->stream, grad, P.n_params, P.theta, P.m, P.v, P.beta_pow, make_hyper(c, 1), 1.f, pid);
+  launch_apply_adam(c->stream, grad, P.n_params, P.theta, P.m, P.v, P.beta_pow, make_hyper(c, 1), 1.f, pid, c->err);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -859,14 +951,16 @@ int ddrl_ppo_update_ddp(ddrl_ctx* c, int pid, const int32_t* shuffle, const int3
     }
   const bool ffn = c->cfg.model_kind == DDRL_MODEL_FFN;
   c->kl_last[pid] = kl;
+  if (ffn && snapshot(c, 1 << pid)) return -1;   // restored by check_err if any step fails
   for (int s = 0; s < steps; ++s) {
+    // test hook: step s's gradient is lost (its Adam launch and every later one skip)
+    if (s == c->fail_step) HIPCHK(hipMemsetD32Async((hipDeviceptr_t)c->err, 1, 1, c->stream));
     if (ffn)
-      launch_update_ffn(c->stream, &ua[s], h, m, inv_n, c->cfg.act_dim, P.d, P.lay.stride, c->cfg.leg_coupling,
-                        c->xchg, c->gx, grad_split(c, m), c->err, &c->upd_epoch);
+      launch_ffn(c, &ua[s], h, m, inv_n, P.d, P.lay.stride, grad_split(c, m), 1);
     else
       launch_step_gnn(c->stream, ua[s], h, 0, m, inv_n, c->gnn, nullptr, c->cfg.gnn_layer);
     NCCLCHK(ncclAllReduce(P.grad, P.grad, (size_t)P.n_params, ncclFloat32, ncclSum, c->comm, c->stream));
-    launch_apply_adam(c->stream, P.grad, P.n_params, P.theta, P.m, P.v, P.beta_pow, h, gscale, pid);
+    launch_apply_adam(c->stream, P.grad, P.n_params, P.theta, P.m, P.v, P.beta_pow, h, gscale, pid, c->err);
   }
   // every rank fails together: a norm-exchange timeout on one rank (whose zeroed gradient has
   // already been summed into every rank's weights) is all-reduced (max) into every rank's

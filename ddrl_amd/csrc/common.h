@@ -80,19 +80,23 @@ __device__ __forceinline__ float tanh_fast(float x) {
   return copysignf(fmaf(-2.f, __builtin_amdgcn_rcpf(e + 1.f), 1.f), x);
 }
 
-// Sum over the 4 lanes that share c (q = 0..3): fixed order ((q0+q1)+(q2+q3)).
-__device__ __forceinline__ float qsum(float v) {
-  v += __shfl_xor(v, 16, 64);
-  v += __shfl_xor(v, 32, 64);
-  return v;
+// Cross-row pair sums with the gfx950 lane-swap instructions (VALU, no LDS round trip like
+// the ds_bpermute a __shfl_xor becomes): v_permlane16_swap_b32 of v with itself leaves rows
+// (0, 0, 2, 2) in one operand and (1, 1, 3, 3) in the other, so their sum is v + v[lane ^ 16];
+// v_permlane32_swap_b32 likewise gives v + v[lane ^ 32].  Every lane gets the same bits as
+// the shuffle form (the two addends are the same, in either order).
+__device__ __forceinline__ float xor16_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xor32_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-// Full wave64 sum, fixed butterfly order.
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
+// Sum over the 4 lanes that share c (q = 0..3): fixed order ((q0+q1)+(q2+q3)).
+__device__ __forceinline__ float qsum(float v) { return xor32_sum(xor16_sum(v)); }
+
 // Sum over the 16 lanes of a DPP row (lanes 16q .. 16q+15, i.e. over c for fixed q), every
 // lane of the row receives the total.  Fixed order: xor 1, xor 2, half-mirror, mirror.
 template <int CTRL>
@@ -106,6 +110,9 @@ __device__ __forceinline__ float row16_sum(float v) {
   v += dpp_mov<0x140>(v);  // row_mirror
   return v;
 }
+
+// Full wave64 sum, fixed order: the DPP row sum, then the rows in pairs (xor 16, xor 32).
+__device__ __forceinline__ float wave_sum(float v) { return qsum(row16_sum(v)); }
 
 // Transpose-reduce: v[0..15] in each lane of a DPP row (16 lanes, index c); afterwards lane c
 // holds the sum over the row of v[c].  Four exchange steps (mirror, half-mirror, quad

@@ -135,12 +135,18 @@ struct UpdateHyper {
 // d / stride: the widest obs width / record stride of the launched policies
 void launch_update_ffn(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n, int A, int d,
                        int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp, int* err,
-                       unsigned* epoch_ctr);   // per-context launch counter (granule tags)
+                       unsigned* epoch_ctr, int* xcc);
+// the same with the relaxed agent-scope atomic exchange (ppo_ffn_atomic.hip): any placement
+void launch_update_ffn_atomic(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n, int A,
+                              int d, int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp,
+                              int* err, unsigned* epoch_ctr, int* xcc);
+// epoch_ctr: per-context launch counter (granule tags)
 size_t gx_bytes(int P);
 // clip_by_global_norm + tf1 Adam on a flat (all-reduced) gradient vector
 // gscale multiplies the gradient before the clip (1 / ranks in the "local" data-parallel mode)
+// err: the context's error word -- a set word (a failed gradient launch) skips the update
 void launch_apply_adam(hipStream_t s, const float* grad, int n, float* theta, float* m, float* v,
-                       float* beta_pow, const UpdateHyper& h, float gscale = 1.f, int xcd = 0);
+                       float* beta_pow, const UpdateHyper& h, float gscale, int xcd, const int* err);
 // Bounds-checked diagnostic build (-DDDRL_BOUNDS): violation counters of the update kernel's
 // staging / record / schedule / LDS indices (see ppo_ffn.hip); ddrl_diag_bounds reads them.
 #define DDRL_NBOUNDS 6

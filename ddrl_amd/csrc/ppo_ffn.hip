@@ -18,1053 +18,8 @@
 //   gradient GEMMs (16x16 tiles, K = 128 rows); per-wave tile ownership;
 //   global-norm clip; tf1 Adam (ApplyAdam) with m / v held in registers by the owning
 //   lane and the weights updated in place in the LDS image.
-#include <atomic>
-#include "common.h"
-#include "kernels.h"
-#include "ffn.h"
-#include "ppo_loss.h"
+#include "ppo_ffn_impl.h"
 
-// Workgroup geometry: NW waves (8 = two per SIMD with one 16-row tile each; the A = 8
-// kernels use 4 waves with two tiles each, their per-wave head partials would not fit LDS).
-// Row split (KSP = 2): each branch runs on two workgroups that take 64 rows of the minibatch
-// each (one 16-row tile per wave, four waves) and swap their partial gradients every step
-// through tagged 8-byte granules; both then hold the same summed gradient and run the same
-// clip + Adam, so their weight images stay bit-identical.
-template <int NW, int ROWS>
-struct Geo {
-  static constexpr int NT = 64 * NW;
-  static constexpr int RT = ROWS / (16 * NW);      // 16-row tiles per wave
-  static constexpr int NS1 = 16 / NW;              // dW2 tile slots per wave (16 tiles)
-  static constexpr int NS2 = (12 + NW - 1) / NW;   // dW1 tile slots per wave (<= 12 tiles)
-};
-__host__ __device__ constexpr int waves_for(int A, int ksp) { return ksp == 2 ? 4 : (A == 8 ? 4 : 8); }
-// value pairs per lane of the partner exchange: small params + stats (padded to a pair),
-// then two per owned dW tile
-// coupling-table slots ("cup" model, models/coupling_net_glorot_uniform_init.py:11-30) among a
-// branch's small parameters: policy branch of the A = 2 kernels
-__host__ __device__ constexpr int ncup_slots(int OB, bool pol) { return pol && OB == 4 ? 2 * OB : 0; }
-__host__ __device__ constexpr int gx_pairs(int OB, int NW) {
-  return ((64 * OB + OB + 128 + ncup_slots(OB, true) + 64 * NW - 1) / (64 * NW) + 2) / 2 + 2 * (16 / NW + (12 + NW - 1) / NW);
-}
-#define GX_MAX_PAIRS 20
-
-struct UpdateBatch {
-  UpdateArgs a[DDRL_MAXP];   // one entry per policy, by value in the kernel argument block
-  UpdateHyper h;
-  int nrows;             // rows per minibatch handled here (<= 128)
-  float inv_n;           // 1 / sgd_minibatch_size (global minibatch)
-  unsigned long long* xchg;  // [P][2 branches][KSP][2 parities] tagged norm^2 granules
-  unsigned long long* gx;    // [P][2 branches][KSP][2 parities][GX_MAX_PAIRS][256 lanes][2] partial-gradient granules
-  int* err;              // set to 1 if an exchange timed out
-  unsigned epoch;        // launch counter (12 bits, never 0): high bits of every exchange tag
-  unsigned lds_bytes;    // dynamic LDS of the launch (bounds-checked build)
-};
-
-// Bounds-checked diagnostic build (-DDDRL_BOUNDS, tools/build_diag.py): every staging,
-// record, schedule and LDS index the update kernel derives at run time is checked against its
-// buffer before use; a violation counts into g_bounds[k] and the access is clamped into range
-// (never faults).  k: 0 staging row of a gathered chunk, 1 record row index >= R, 2 schedule
-// index (perm / shuffle) out of range, 3 LDS-DMA destination past the launch's LDS, 4 staged
-// record read past the staging rows, 5 parameter index past n_params.
-#ifdef DDRL_BOUNDS
-__device__ unsigned g_bounds[DDRL_NBOUNDS];
-__device__ __forceinline__ bool bchk(bool ok, int k) {
-  if (!ok) atomicAdd(&g_bounds[k], 1u);
-  return ok;
-}
-extern "C" int ddrl_diag_bounds(unsigned* host, int reset) {
-  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bounds), sizeof(g_bounds)) != hipSuccess) return -1;
-  if (reset) {
-    unsigned z[DDRL_NBOUNDS] = {0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_bounds), z, sizeof(z)) != hipSuccess) return -1;
-  }
-  return 0;
-}
-#define BCHK(cond, k) bchk((cond), (k))
-#else
-#define BCHK(cond, k) true
-#endif
-// Exchange tag of a step: the launch epoch above the step count, so a granule line some
-// cache still holds from an earlier launch can never carry a tag of this one.
-__device__ __forceinline__ unsigned xchg_tag(unsigned epoch, int step) {
-  return (epoch << 20) | (((unsigned)step + 1u) & 0xfffffu);
-}
-
-// Per-branch view of the flat (Keras-order) parameter vector.
-struct BranchOff { int w1, b1, w2, b2, wo, bo, cup; };
-__device__ __forceinline__ BranchOff branch_off(const FfnOffsets& o, bool pol) {
-  BranchOff b;
-  b.cup = o.n;   // "cup" model: the leg-coupling table [4][A] follows the fcnet variables
-  b.w1 = pol ? o.w1 : o.vw1; b.b1 = pol ? o.b1 : o.vb1;
-  b.w2 = pol ? o.w2 : o.vw2; b.b2 = pol ? o.b2 : o.vb2;
-  b.wo = pol ? o.wo : o.vo;  b.bo = pol ? o.bo : o.vbo;
-  return b;
-}
-
-template <int OB>
-__device__ void stage_branch(const float* __restrict__ th, int d, const BranchOff& bo, float* lds,
-                             NetLds& W, int ncup) {
-  W.w1 = lds; W.w2 = W.w1 + 48 * 64; W.b1 = W.w2 + 64 * 64; W.b2 = W.b1 + 64;
-  W.wo = W.b2 + 64; W.bo = W.wo + 64 * OB; W.cup = W.bo + OB;   // cup: OB <= 4 (A = 2)
-  for (int i = threadIdx.x; i < ncup; i += blockDim.x) W.cup[i] = th[bo.cup + i];
-  for (int i = threadIdx.x; i < 48 * 64; i += blockDim.x) {
-    const int f = i >> 6;
-    W.w1[sidx(f, i & 63)] = f < d ? th[bo.w1 + i] : 0.f;
-  }
-  for (int i = threadIdx.x; i < 64 * 64; i += blockDim.x) W.w2[sidx(i >> 6, i & 63)] = th[bo.w2 + i];
-  for (int i = threadIdx.x; i < 64; i += blockDim.x) { W.b1[i] = th[bo.b1 + i]; W.b2[i] = th[bo.b2 + i]; }
-  for (int i = threadIdx.x; i < 64 * OB; i += blockDim.x) W.wo[i] = th[bo.wo + i];
-  for (int i = threadIdx.x; i < OB; i += blockDim.x) W.bo[i] = th[bo.bo + i];
-}
-// The same image with every weight load of a thread issued before the first LDS store (one
-// memory round trip instead of one per loop trip; NT = threads per workgroup, 256 or 512).
-template <int OB, int NT>
-__device__ __forceinline__ void stage_branch_batched(const float* __restrict__ th, int d, const BranchOff& bo,
-                                                     float* lds, NetLds& W, int ncup) {
-  static_assert((48 * 64) % NT == 0 && (64 * 64) % NT == 0, "staging split");
-  constexpr int N1 = 48 * 64 / NT, N2 = 64 * 64 / NT, NS = (64 * OB + OB + 128 + NT - 1) / NT;
-  W.w1 = lds; W.w2 = W.w1 + 48 * 64; W.b1 = W.w2 + 64 * 64; W.b2 = W.b1 + 64;
-  W.wo = W.b2 + 64; W.bo = W.wo + 64 * OB; W.cup = W.bo + OB;
-  const int t = threadIdx.x;
-  float a1[N1], a2[N2], as[NS];
-#pragma unroll
-  for (int k = 0; k < N1; ++k) {
-    const int i = t + NT * k;
-    a1[k] = (i >> 6) < d ? th[bo.w1 + i] : 0.f;
-  }
-#pragma unroll
-  for (int k = 0; k < N2; ++k) a2[k] = th[bo.w2 + t + NT * k];
-#pragma unroll
-  for (int k = 0; k < NS; ++k) {   // [wo 64 OB][bo OB][b1 64][b2 64]
-    int e = t + NT * k;
-    float x = 0.f;
-    if (e < 64 * OB) x = th[bo.wo + e];
-    else if ((e -= 64 * OB) < OB) x = th[bo.bo + e];
-    else if ((e -= OB) < 64) x = th[bo.b1 + e];
-    else if ((e -= 64) < 64) x = th[bo.b2 + e];
-    as[k] = x;
-  }
-  float ac = t < ncup ? th[bo.cup + t] : 0.f;   // ncup <= 8 < NT
-#pragma unroll
-  for (int k = 0; k < N1; ++k) {
-    const int i = t + NT * k;
-    W.w1[sidx(i >> 6, i & 63)] = a1[k];
-  }
-#pragma unroll
-  for (int k = 0; k < N2; ++k) {
-    const int i = t + NT * k;
-    W.w2[sidx(i >> 6, i & 63)] = a2[k];
-  }
-#pragma unroll
-  for (int k = 0; k < NS; ++k) {
-    int e = t + NT * k;
-    if (e < 64 * OB) W.wo[e] = as[k];
-    else if ((e -= 64 * OB) < OB) W.bo[e] = as[k];
-    else if ((e -= OB) < 64) W.b1[e] = as[k];
-    else if ((e -= 64) < 64) W.b2[e] = as[k];
-  }
-  if (t < ncup) W.cup[t] = ac;
-}
-#define BRANCH_LDS_FLOATS (48 * 64 + 64 * 64 + 128 + 64 * 16 + 16)   // multiple of 4 floats
-
-// "Small" parameters owned one per thread: [dWo 64*OB][dbo OB][db1 64][db2 64], then the
-// policy branch's leg-coupling table [4][A] of the "cup" model
-template <int OB>
-__device__ __forceinline__ void small_param(int e, const BranchOff& bo, const NetLds& W, int& pidx, float*& lp) {
-  if (e < 64 * OB) { pidx = bo.wo + e; lp = W.wo + e; return; }
-  e -= 64 * OB;
-  if (e < OB) { pidx = bo.bo + e; lp = W.bo + e; return; }
-  e -= OB;
-  if (e < 64) { pidx = bo.b1 + e; lp = W.b1 + e; return; }
-  e -= 64;
-  if (e < 64) { pidx = bo.b2 + e; lp = W.b2 + e; return; }
-  e -= 64;
-  pidx = bo.cup + e; lp = W.cup + e;
-}
-
-
-template <int A, int RT>
-struct RowData {
-  float x[RT][12];      // this wave's row tiles
-  float act[RT][A];
-  float ol[RT][2 * A];
-  float s0[RT], s1[RT];  // policy: logp_old, adv;  value: vf_old, vt
-  int cid[RT];           // "cup": coupling row of the record
-};
-
-// The next minibatch's 128 records are gathered by LDS-DMA into stg [128][stride] while the
-// current step computes: 16-byte chunk g of the gather is record column 4 (g % cpr) of row
-// g / cpr (cpr = stride / 4), and one wave-instruction writes 64 consecutive chunks (the
-// lane-linear LDS destination of global_load_lds).  Whole 64-byte record lines instead of
-// per-lane dword gathers: 3 line requests per row rather than one per field and lane.
-// The staging rows hold cpr_l = cpr | 1 chunks (an odd number: the 16 rows a lane group
-// reads then start in 16 different banks); the pad chunk repeats the row's last chunk.
-// Issued by waves 0 .. NW-2: the last wave keeps its vector-memory counter free for the
-// norm exchange (an early partner poll would otherwise wait for the gathers too).
-template <int NW, int ROWS>
-__device__ __forceinline__ void issue_rows(const float* rec, int stride, int cpr, int cpr_l, const int* idxb,
-                                           float* stg, int R, unsigned lds_bytes) {
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
-  if (w == NW - 1) return;
-  const int nchunk = ROWS * cpr_l;
-  const float inv = 1.f / (float)cpr_l;
-  for (int base = 64 * w; base < nchunk; base += 64 * (NW - 1)) {   // wave-uniform
-    const int g = base + lane;
-    int row = (int)(((float)g + 0.5f) * inv);
-    const int k = min(g - row * cpr_l, cpr - 1);
-    const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr(stg + 4 * base));
-    if (g < nchunk) {
-      if (!BCHK(row >= 0 && row < ROWS && k >= 0, 0)) row = 0;
-      int idx = idxb[row];
-      if (!BCHK(idx >= 0 && idx < R, 1)) idx = 0;
-      if (BCHK(dst + 16u * (unsigned)lane + 16u <= lds_bytes, 3))
-        glds16(rec + (size_t)idx * stride + 4 * k, dst);
-    }
-  }
-  (void)R; (void)lds_bytes;
-}
-
-// staging-row chunks for a record of `stride` floats (the A = 8 kernels keep the plain
-// stride: their LDS budget has no room for the pad)
-__host__ __device__ constexpr int stg_chunks(int stride, int A) { return A == 8 ? stride / 4 : (stride / 4) | 1; }
-
-// This lane's rows from the staged records (padding rows hold record 0; their output
-// gradient is zeroed).  Observation columns f >= d are zero (they meet the zero rows of the
-// W1 image; their dW1 rows are never stored): the generic KS1 = 12 instance (d of no exact
-// instance, e.g. the LegID env's 23) would otherwise read past the record -- past the staging
-// buffer for the last row, whatever that LDS holds -- and 0 x NaN is NaN.
-template <int A, int KS1, bool POL, int RT>
-__device__ __forceinline__ void load_row(const float* stg, int stg_stride, const RecLayout& L, const int* row_l,
-                                         int d, RowData<A, RT>& r) {
-  const int q = (threadIdx.x & 63) >> 4;
-#ifdef DDRL_BOUNDS
-  {
-    // the widest column this lane group reads (the generic KS1 = 12 instance reads columns < d
-    // only): it must lie inside the record, i.e. inside this row's staging slot
-    int hi = KS1 < 12 ? L.obs + 4 * KS1 - 1 : L.obs + d - 1;
-    if (POL) hi = max(max(hi, L.act + A - 1), max(L.logit + 2 * A - 1, max(L.logp, max(L.adv, L.cid))));
-    else hi = max(hi, max(L.vf, L.vt));
-    for (int t = 0; t < RT; ++t) BCHK(row_l[t] >= 0 && row_l[t] < DDRL_MB && hi < L.stride, 4);
-  }
-#endif
-#pragma unroll
-  for (int t = 0; t < RT; ++t) {
-    const float* rp = stg + row_l[t] * stg_stride;
-#pragma unroll
-    for (int s = 0; s < 12; ++s)   // exact instances (KS1 = ceil(d / 4)) stay inside the record
-      r.x[t][s] = (s < KS1 && (KS1 < 12 || 4 * s + q < d)) ? rp[L.obs + 4 * s + q] : 0.f;
-    if (POL) {
-#pragma unroll
-      for (int j = 0; j < A; ++j) r.act[t][j] = rp[L.act + j];
-#pragma unroll
-      for (int j = 0; j < 2 * A; ++j) r.ol[t][j] = rp[L.logit + j];
-      r.s0[t] = rp[L.logp];
-      r.s1[t] = rp[L.adv];
-      r.cid[t] = L.cid >= 0 ? min(max((int)rp[L.cid], 0), 3) : 0;
-    } else {
-      r.cid[t] = 0;
-#pragma unroll
-      for (int j = 0; j < A; ++j) r.act[t][j] = 0.f;
-#pragma unroll
-      for (int j = 0; j < 2 * A; ++j) r.ol[t][j] = 0.f;
-      r.s0[t] = rp[L.vf];
-      r.s1[t] = rp[L.vt];
-    }
-  }
-}
-
-// Per-step learner statistics from the per-wave partial sums red[w * 8 + k]: policy
-// workgroup -> policy_loss, kl, entropy; value workgroup -> vf_loss, vf_explained_var.
-template <bool POL, int NSTAT, int NW, int KSP>
-__device__ __forceinline__ void write_stats(float* so, const float* red, float n) {
-  float sv[NSTAT];
-#pragma unroll
-  for (int k = 0; k < NSTAT; ++k) {
-    if constexpr (KSP == 2) {
-      sv[k] = red[96 + k];   // both workgroups' sums, combined at the exchange
-    } else {
-      sv[k] = 0.f;
-      for (int i = 0; i < NW; ++i) sv[k] += red[i * 8 + k];
-    }
-  }
-  if constexpr (POL) {
-    gst(so + 1, sv[0] / n); gst(so + 3, sv[1] / n); gst(so + 4, sv[2] / n);
-  } else {
-    gst(so + 2, sv[0] / n);
-    const float vy = sv[2] / n - (sv[1] / n) * (sv[1] / n);
-    const float vd = sv[4] / n - (sv[3] / n) * (sv[3] / n);
-    gst(so + 5, vy > 0.f ? fmaxf(-1.f, 1.f - vd / vy) : 0.f);
-  }
-}
-
-__device__ __forceinline__ int row_index(const UpdateArgs& U, int step, int row_l, bool ok) {
-  if (!ok) return 0;
-  const int e = step / U.nb, b = step - e * U.nb;
-#ifdef DDRL_BOUNDS
-  if (!BCHK(e >= 0 && e < U.n_epochs, 2)) return 0;
-  const int slot = gld(U.perm + e * U.nb + b);
-  if (!BCHK(slot >= 0 && slot < U.nb && (slot + 1) * DDRL_MB <= max(U.R, DDRL_MB) && row_l < DDRL_MB, 2)) return 0;
-  return gld(U.shuffle + slot * DDRL_MB + row_l);
-#else
-  return gld(U.shuffle + gld(U.perm + e * U.nb + b) * DDRL_MB + row_l);
-#endif
-}
-// minibatch slot of a step (wave-uniform: perm[e][b])
-__device__ __forceinline__ int perm_slot(const UpdateArgs& U, int step) {
-  const int e = step / U.nb, b = step - e * U.nb;
-  return gld(U.perm + e * U.nb + b);
-}
-
-// Diagnostic build only (-DDDRL_STAMPS): per-phase s_memtime cycle counts of wave 0 of each
-// workgroup, accumulated over the steps of one launch; no stamp executes in the real build.
-#ifdef DDRL_STAMPS
-__device__ unsigned long long g_stamps[32][16];
-#define STAMP_INIT unsigned long long st_prev = __builtin_amdgcn_s_memtime(), st_acc[16] = {0};
-#define STAMP(k) do { if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[k] += t_ - st_prev; st_prev = t_; } } while (0)
-#define STAMP_DONE do { if (tid == 0) for (int k_ = 0; k_ < 16; ++k_) g_stamps[blockIdx.x][k_] = st_acc[k_]; } while (0)
-extern "C" int ddrl_diag_stamps(unsigned long long* host) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) == hipSuccess ? 0 : -1;
-}
-#else
-#define STAMP_INIT
-#define STAMP(k)
-#define STAMP_DONE
-#endif
-
-// Partner exchange of the row split: 16-byte granules {value, tag, value, tag} (each 8-byte
-// half carries the step tag, so a half is valid exactly when its tag matches: no fence),
-// written by one sc1 (write-through) buffer store and read by one sc1 buffer load; the
-// outboxes are double buffered by step parity and cleared before each launch.  Pair j of
-// lane l sits at box[(j * 256 + l) * 16 bytes] (coalesced per pair).
-// Cache policy of the exchange (gfx950 CPol bits: sc0 = 1, nt = 2, sc1 = 16).  The four
-// workgroups of a policy share one XCD and hence one L2 (blocks b, b + 8, ... are dealt to
-// XCD b mod 8; tools/xchg_bench.hip prints the placement).  Plain stores write through the
-// per-CU L1 into that L2 and stay there; the poller's sc1 (device-scope) loads miss its own
-// L1.  Measured one-hop latency (tools/xchg_bench.hip, MI355X): plain store / sc1 load
-// 0.24 us, sc1 store / sc1 load 0.50 us (the sc1 store writes through to memory), sc0 loads
-// never see the partner (they hit the stale L1 line).
-#ifndef DDRL_GX_ST
-#define DDRL_GX_ST 0
-#endif
-#ifndef DDRL_GX_LD
-#define DDRL_GX_LD 16
-#endif
-#ifndef DDRL_GX_INV
-#define DDRL_GX_INV 0
-#endif
-__device__ __forceinline__ void xchg_inv_l1() {
-#if DDRL_GX_INV
-  asm volatile("buffer_inv sc0" ::: "memory");
-#endif
-}
-// Once any exchange has waited this long (100 MHz ticks), the waiter also polls the error
-// word, so one timed-out exchange ends every later wait at once instead of each one
-// spinning to its own timeout.
-#define XCHG_SLOW_TICKS 20000ull        // 200 us
-#define XCHG_TIMEOUT_TICKS 300000000ull // 3 s
-__device__ __forceinline__ bool xchg_abandon(unsigned long long t0, int* err) {
-  const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
-  if (dt < XCHG_SLOW_TICKS) return false;
-  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return true;
-  if (dt > XCHG_TIMEOUT_TICKS) { atomicExch(err, 1); return true; }
-  return false;
-}
-// Two builds of the same protocol:
-//  * default: plain stores into the XCD's shared L2 and sc1 polls (0.24 us per hop); correct
-//    when the workgroups that exchange share an L2.  The dispatcher deals a grid's blocks to
-//    the 8 XCDs round robin, from a start XCD that varies between dispatches (measured: a
-//    data-parallel gradient launch found block p on XCD != p), so blocks b = p mod 8 -- the
-//    workgroups of policy p -- always share one XCD.  Were that ever broken, a poll would
-//    never see its partner: the 3 s bound raises the error word and the host names the
-//    atomic build.  With coh set the stores are sc1 (device-coherent write-through: the ISA
-//    of a relaxed agent-scope atomic store), 0.50 us per hop.
-//  * -DDDRL_XCHG_ATOMIC: every granule access is a relaxed agent-scope 64-bit atomic
-//    (__hip_atomic_load / __hip_atomic_store): defined behaviour under the HIP memory model
-//    for any placement, each 8-byte {value, tag} half its own atomic.  The bounds-checked
-//    diagnostic library is built this way, so the GPU suite runs the update under both.
-#ifdef DDRL_XCHG_ATOMIC
-typedef unsigned long long* gx_box_t;
-__device__ __forceinline__ gx_box_t gx_rsrc(unsigned long long* box) { return box; }
-__device__ __forceinline__ void gx_put(gx_box_t r, int j, float v0, float v1, unsigned tag, bool) {
-  unsigned long long* g = r + 2 * (j * 256 + (int)threadIdx.x);
-  __hip_atomic_store(g, ((unsigned long long)tag << 32) | __float_as_uint(v0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(g + 1, ((unsigned long long)tag << 32) | __float_as_uint(v1), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void xchg_store(unsigned long long* g, unsigned long long v, bool) {
-  __hip_atomic_store(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long xchg_load(unsigned long long* g) {
-  return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <int NP, typename F>
-__device__ __forceinline__ void gx_get(gx_box_t r, unsigned tag, float* out, int* err, F&& after_first) {
-  unsigned long long g[2 * NP];
-  unsigned long long* b = r + 2 * (int)threadIdx.x;
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  bool first = true;
-  for (;;) {
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      g[2 * j] = __hip_atomic_load(b + 512 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      g[2 * j + 1] = __hip_atomic_load(b + 512 * j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (first) { after_first(); first = false; }
-    bool ok = true;
-#pragma unroll
-    for (int j = 0; j < 2 * NP; ++j) ok = ok && (unsigned)(g[j] >> 32) == tag;
-    if (ok) break;
-    if (xchg_abandon(t0, err)) {
-#pragma unroll
-      for (int j = 0; j < 2 * NP; ++j) g[j] = 0ull;
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-#pragma unroll
-  for (int j = 0; j < 2 * NP; ++j) out[j] = __uint_as_float((unsigned)g[j]);
-}
-#else
-typedef __amdgpu_buffer_rsrc_t gx_box_t;
-__device__ __forceinline__ gx_box_t gx_rsrc(unsigned long long* box) {
-  return __builtin_amdgcn_make_buffer_rsrc(box, 0, GX_MAX_PAIRS * 256 * 16, 0x00020000);
-}
-__device__ __forceinline__ void gx_put(gx_box_t r, int j, float v0, float v1, unsigned tag, bool coh) {
-  const v4u g = {__float_as_uint(v0), tag, __float_as_uint(v1), tag};
-  if (coh) __builtin_amdgcn_raw_buffer_store_b128(g, r, (j * 256 + (int)threadIdx.x) * 16, 0, 16);
-  else __builtin_amdgcn_raw_buffer_store_b128(g, r, (j * 256 + (int)threadIdx.x) * 16, 0, DDRL_GX_ST);
-}
-// Norm granule (8 bytes: tag << 32 | value), one 64-bit access each way, same policy.
-__device__ __forceinline__ void xchg_store(unsigned long long* g, unsigned long long v, bool coh) {
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(g, 0, 8, 0x00020000);
-  typedef unsigned v2u_t __attribute__((ext_vector_type(2)));
-  const v2u_t x = {(unsigned)v, (unsigned)(v >> 32)};
-  if (coh) __builtin_amdgcn_raw_buffer_store_b64(x, r, 0, 0, 16);
-  else __builtin_amdgcn_raw_buffer_store_b64(x, r, 0, 0, DDRL_GX_ST);
-}
-__device__ __forceinline__ unsigned long long xchg_load(unsigned long long* g) {
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(g, 0, 8, 0x00020000);
-  typedef unsigned v2u_t __attribute__((ext_vector_type(2)));
-  xchg_inv_l1();
-  const v2u_t x = __builtin_amdgcn_raw_buffer_load_b64(r, 0, 0, DDRL_GX_LD);
-  return ((unsigned long long)x[1] << 32) | x[0];
-}
-// The partner's NP pairs of this lane: all loads in flight, re-polled until every tag
-// matches; bounded (a timeout flags err and returns zeros).
-template <int NP, typename F>
-__device__ __forceinline__ void gx_get(gx_box_t r, unsigned tag, float* out, int* err, F&& after_first) {
-  v4u g[NP];
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  bool first = true;
-  for (;;) {
-    xchg_inv_l1();
-#pragma unroll
-    for (int j = 0; j < NP; ++j) g[j] = __builtin_amdgcn_raw_buffer_load_b128(r, (j * 256 + (int)threadIdx.x) * 16, 0, DDRL_GX_LD);
-    if (first) { after_first(); first = false; }
-    bool ok = true;
-#pragma unroll
-    for (int j = 0; j < NP; ++j) ok = ok && g[j][1] == tag && g[j][3] == tag;
-    if (ok) break;
-    if (xchg_abandon(t0, err)) {
-#pragma unroll
-      for (int j = 0; j < NP; ++j) g[j] = v4u{0u, 0u, 0u, 0u};
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-#pragma unroll
-  for (int j = 0; j < NP; ++j) {
-    out[2 * j] = __uint_as_float(g[j][0]);
-    out[2 * j + 1] = __uint_as_float(g[j][2]);
-  }
-}
-#endif
-
-template <int A, int KS1, int OB, bool POL, int NW, int KSP, bool CUP>
-__device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBatch& ub, float* lds, int p, int kq) {
-  constexpr int ROWS = DDRL_MB / KSP;
-  constexpr int NT = Geo<NW, ROWS>::NT, RT = Geo<NW, ROWS>::RT, NS1 = Geo<NW, ROWS>::NS1, NS2 = Geo<NW, ROWS>::NS2;
-  const UpdateHyper& H = ub.h;
-  const int d = U.d;
-  const FfnOffsets of = ffn_offsets(d, A);
-  const BranchOff bo = branch_off(of, POL);
-  const int nf1 = (d + 15) >> 4;
-  constexpr int NSB0 = 64 * OB + OB + 128;         // small params of this branch
-  constexpr int NCUP = CUP ? ncup_slots(OB, POL) : 0;   // + the "cup" coupling table
-  constexpr int NSB = NSB0 + NCUP;                  // small params of this branch
-  constexpr bool cup = NCUP > 0;
-  constexpr int nsb = NSB;
-  constexpr int NSLOT = (NSB + NT - 1) / NT;
-  constexpr int NSTAT = POL ? 3 : 5;
-  constexpr int NTS = NS1 + NS2;
-  constexpr int NP0 = (NSLOT + 2) / 2;              // exchange pairs: small params + stats,
-  constexpr int NP = NP0 + 2 * NTS;                  // then the owned dW tiles (KSP = 2)
-  static_assert(KSP == 1 || (NT == 256 && NP == gx_pairs(OB, NW) && NP <= GX_MAX_PAIRS), "exchange pairs");
-
-  NetLds W;
-  constexpr int LD = ROWS + 8;              // feature-major image stride
-  float* bufA = lds + BRANCH_LDS_FLOATS;    // feature-major [64][LD]: H1, then X
-  float* bufB = bufA + 64 * LD;             // feature-major [64][LD]: dZ2, then dZ1
-  float* Pb = bufB + 64 * LD;               // [NW][NSB] per-wave partial small grads
-  float* red = Pb + NW * NSB;               // [NW][8] row-stat partials, [64..] scalars
-  int* idxb = reinterpret_cast<int*>(red + 128);   // [128] record rows of the next step
-  float* stg = red + 256;                   // [ROWS][stride] records of the next step (16 B aligned)
-  const int stride = U.lay.stride, cpr = stride >> 2, cpr_l = stg_chunks(stride, A);
-
-  // w is wave-uniform: readfirstlane keeps it (and the tile indices derived from it) in SGPRs
-  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, q = lane >> 4,
-            w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // Store cache policy of the exchange.  A run-time choice here cost 0.3 us per step (the
-  // branches around every granule store, measured), so the device-coherent protocol is the
-  // separate -DDDRL_XCHG_ATOMIC build and this one always stores plainly into the XCD's L2.
-  constexpr bool coh = false;
-  int row_l[RT];
-  bool row_ok[RT];
-#pragma unroll
-  for (int t = 0; t < RT; ++t) {
-    row_l[t] = 16 * RT * w + 16 * t + c;               // row of this workgroup's share
-    row_ok[t] = ROWS * kq + row_l[t] < ub.nrows;
-  }
-
-  // ---- first step's records (LDS-DMA) in flight while the weights are staged ----
-  const int total_steps = U.n_epochs * U.nb;
-  const int last = U.max_steps >= 0 ? min(total_steps, U.step0 + U.max_steps) : total_steps;
-  // minibatch row of this lane's staging slot (tid < ROWS)
-  const int gr = ROWS * kq + tid;
-  const bool gok = tid < ROWS && gr < ub.nrows;
-  if (tid < ROWS) idxb[tid] = U.step0 < last && gok ? row_index(U, U.step0, gr, true) : 0;
-  __syncthreads();
-  if (U.step0 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, idxb, stg, U.R, ub.lds_bytes);
-  stage_branch_batched<OB, NT>(U.theta, d, bo, lds, W, NCUP);
-
-  // ---- optimizer state of the parameters this lane owns ----
-  // tile tt = 4 fa + fo; slots 0..NS1-1: dW2 tiles w + NW i;  then dW1 tiles w + NW i (if < 4 nf1).
-  // NW is a multiple of 4, so every tile of a wave has fo = w & 3.
-  floatx4 mt[NTS], vt4[NTS];
-  bool tv[NTS];
-  int tfa[NTS], tfo[NTS];
-#pragma unroll
-  for (int i = 0; i < NTS; ++i) {
-    const int tt = i < NS1 ? w + NW * i : w + NW * (i - NS1);
-    tv[i] = i < NS1 ? true : (tt < 4 * nf1);
-    tfa[i] = tt >> 2;
-    tfo[i] = tt & 3;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int f = 16 * tfa[i] + 4 * q + r, o = 16 * tfo[i] + c;
-      const bool ok = tv[i] && (i < NS1 || f < d) && !U.grad_out;   // gradient-only launches: no Adam
-      const int pidx = (i < NS1 ? bo.w2 : bo.w1) + f * 64 + o;
-      BCHK(!ok || (pidx >= 0 && pidx < of.n), 5);
-      mt[i][r] = ok ? U.m[pidx] : 0.f;
-      vt4[i][r] = ok ? U.v[pidx] : 0.f;
-
-    }
-  }
-  float ms[NSLOT], vs[NSLOT];
-#pragma unroll
-  for (int k = 0; k < NSLOT; ++k) {
-    const int e = tid + NT * k;
-    ms[k] = vs[k] = 0.f;
-    if (e < nsb && !U.grad_out) {
-      int pidx; float* lp;
-      small_param<OB>(e, bo, W, pidx, lp);
-      BCHK(pidx >= 0 && pidx < of.n + NCUP, 5);
-      ms[k] = U.m[pidx];
-      vs[k] = U.v[pidx];
-    }
-  }
-  int ebase[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) ebase[r] = sidx(4 * q + r, 16 * (w & 3) + c);
-  float b1p = U.beta_pow[0], b2p = U.beta_pow[1];
-  const float adv_mean = U.adv_norm[0], adv_den = U.adv_norm[1];
-  const float beta = U.kl_coeff;
-  const float lo = 1.f - H.clip, hi = 1.f + H.clip;
-  __syncthreads();
-
-  RowData<A, RT> cur;
-  // records of step0 -> stg (issued above), row indices of step0 + 1 -> idxb, of step0 + 2 -> nxt
-  wait_vmcnt0();
-  __syncthreads();
-  if (tid < ROWS) idxb[tid] = U.step0 + 1 < last && gok ? row_index(U, U.step0 + 1, gr, true) : 0;
-  int nxt = U.step0 + 2 < last && gok ? row_index(U, U.step0 + 2, gr, true) : 0;
-  // partner exchange slots: mine / the other row half of this branch, by step parity
-  const size_t gx_branch = ((size_t)p * 2 + (POL ? 0 : 1)) * KSP;
-  __syncthreads();
-
-  STAMP_INIT
-  for (int step = U.step0; step < last; ++step) {
-    load_row<A, KS1, POL, RT>(stg, 4 * cpr_l, U.lay, row_l, d, cur);
-    // ---- forward + loss + output gradient (two row tiles) ----
-    floatx4 h1[RT][4], h2[RT][4], dz[RT][4];
-    float out[RT][OB], dout[RT][OB];
-    ffn_fwd_rt<OB, KS1, RT>(W, cur.x, h1, h2, out);
-    // "cup" (coupling_net_glorot_uniform_init.py:22-30): means scaled by the record's leg row
-    float pre[RT][A], cf[RT][A];
-    if constexpr (cup) {
-      {
-#pragma unroll
-        for (int t = 0; t < RT; ++t)
-#pragma unroll
-          for (int j = 0; j < A; ++j) {
-            pre[t][j] = out[t][j];
-            cf[t][j] = W.cup[cur.cid[t] * A + j];
-            out[t][j] *= cf[t][j];
-          }
-      }
-    }
-    STAMP(0);
-    float st[NSTAT];
-#pragma unroll
-    for (int k = 0; k < NSTAT; ++k) st[k] = 0.f;
-#pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      float st0[NSTAT];
-      if constexpr (POL)
-        policy_loss_row<A>(out[t], cur.act[t], cur.ol[t], cur.s0[t], (cur.s1[t] - adv_mean) / adv_den,
-                           beta, lo, hi, H.ent_coeff, ub.inv_n, row_ok[t], dout[t], st0);
-      else
-        value_loss_row(out[t][0], cur.s0[t], cur.s1[t], H, ub.inv_n, row_ok[t], dout[t], st0);
-#pragma unroll
-      for (int k = 0; k < NSTAT; ++k) st[k] += st0[k];
-    }
-    STAMP(1);
-    float* Pw = Pb + w * NSB;
-    if constexpr (cup) {
-      {
-        // d coupling[leg][j] = sum over the leg's rows of dmean_j * pre-coupling mean_j;
-        // the fcnet head then sees dmean_j * coupling[leg][j]
-#pragma unroll
-        for (int lg = 0; lg < 4; ++lg)
-#pragma unroll
-          for (int j = 0; j < A; ++j) {
-            float v = 0.f;
-#pragma unroll
-            for (int t = 0; t < RT; ++t) v += cur.cid[t] == lg ? dout[t][j] * pre[t][j] : 0.f;
-            v = row16_sum(v);
-            if (lane == 0) Pw[NSB0 + lg * A + j] = v;
-          }
-#pragma unroll
-        for (int t = 0; t < RT; ++t)
-#pragma unroll
-          for (int j = 0; j < A; ++j) dout[t][j] *= cf[t][j];
-      }
-    }
-    // head weight / bias partial gradients over this wave's rows: DPP transpose-reduce
-    // of the 16 features (fb, r) a lane holds; afterwards lane (c, q) owns feature
-    // h = 16 (c >> 2) + 4 q + (c & 3).
-    const int h_own = 16 * (c >> 2) + 4 * q + (c & 3);
-#ifndef DDRL_ABL_NO_HEADDPP
-#pragma unroll
-    for (int o = 0; o < OB; ++o) {
-      float v[16];
-#pragma unroll
-      for (int fb = 0; fb < 4; ++fb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[4 * fb + r] = h2[0][fb][r] * dout[0][o];
-#pragma unroll
-          for (int t = 1; t < RT; ++t) v[4 * fb + r] += h2[t][fb][r] * dout[t][o];
-        }
-      Pw[h_own * OB + o] = row16_transpose_sum(v);
-    }
-#endif
-#pragma unroll
-    for (int o = 0; o < OB; ++o) {
-      float dsum = dout[0][o];
-#pragma unroll
-      for (int t = 1; t < RT; ++t) dsum += dout[t][o];
-      const float s = row16_sum(dsum);
-      if (lane == 0) Pw[64 * OB + o] = s;
-    }
-#pragma unroll
-    for (int k = 0; k < NSTAT; ++k) {
-      const float s = row16_sum(st[k]);
-      if (lane == 0) red[w * 8 + k] = s;
-    }
-    STAMP(2);
-#pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      head_bwd<OB>(W, dout[t], dz[t]);
-      dtanh_inplace(dz[t], h2[t]);                       // dz = dZ2
-    }
-    {
-      float v[16];
-#pragma unroll
-      for (int fb = 0; fb < 4; ++fb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[4 * fb + r] = dz[0][fb][r];
-#pragma unroll
-          for (int t = 1; t < RT; ++t) v[4 * fb + r] += dz[t][fb][r];
-        }
-      Pw[64 * OB + OB + 64 + h_own] = row16_transpose_sum(v);     // db2
-    }
-#pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      store_act_fm<LD>(bufA, RT * w + t, h1[t]);
-      store_act_fm<LD>(bufB, RT * w + t, dz[t]);
-    }
-    STAMP(3);
-#ifndef DDRL_ABL_NO_L2BWD
-    layer2_bwd_rt<RT>(W, dz, h2);                        // h2 <- dH1
-#endif
-#pragma unroll
-    for (int t = 0; t < RT; ++t) dtanh_inplace(h2[t], h1[t]);  // h2 = dZ1
-    {
-      float v[16];
-#pragma unroll
-      for (int fb = 0; fb < 4; ++fb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[4 * fb + r] = h2[0][fb][r];
-#pragma unroll
-          for (int t = 1; t < RT; ++t) v[4 * fb + r] += h2[t][fb][r];
-        }
-      Pw[64 * OB + OB + h_own] = row16_transpose_sum(v);          // db1
-    }
-    STAMP(4);
-    __syncthreads();                                     // #1: H1, dZ2, partials visible
-    STAMP(5);
-    const unsigned gtag = xchg_tag(ub.epoch, step);
-    const size_t gx_box = (size_t)GX_MAX_PAIRS * 256 * 2;   // granules per outbox
-    const gx_box_t gx_mine = gx_rsrc(ub.gx + ((gx_branch + kq) * 2 + (step & 1)) * gx_box);
-    float gs[NSLOT];
-    float st_own = 0.f;
-    if constexpr (KSP == 2) {
-      // small-parameter partials and this half's loss statistics go out first
-      float v0[2 * NP0];
-#pragma unroll
-      for (int k = 0; k < 2 * NP0; ++k) v0[k] = 0.f;
-#pragma unroll
-      for (int k = 0; k < NSLOT; ++k) {
-        const int e = tid + NT * k;
-        float sm = 0.f;
-        if (e < nsb)
-          for (int i = 0; i < NW; ++i) sm += Pb[i * NSB + e];
-        gs[k] = sm;
-        v0[k] = sm;
-      }
-      if (tid < NSTAT)
-        for (int i = 0; i < NW; ++i) st_own += red[i * 8 + tid];
-      v0[NSLOT] = st_own;
-#pragma unroll
-      for (int j = 0; j < NP0; ++j) gx_put(gx_mine, j, v0[2 * j], v0[2 * j + 1], gtag, coh);
-    }
-    floatx4 gt[NTS];
-#ifndef DDRL_ABL_NO_DW2   // ablation builds (timing only): skip a phase
-    dw_tiles_fm<ROWS, NS1>(bufA, bufB, tfa, w & 3, gt);   // dW2 tiles of this wave
-#else
-    for (int i = 0; i < NS1; ++i) gt[i] = splat4(0.f);
-#endif
-    if constexpr (KSP == 2) {
-#pragma unroll
-      for (int i = 0; i < NS1; ++i) {
-        gx_put(gx_mine, NP0 + 2 * i, gt[i][0], gt[i][1], gtag, coh);
-        gx_put(gx_mine, NP0 + 2 * i + 1, gt[i][2], gt[i][3], gtag, coh);
-      }
-    }
-    STAMP(6);
-    __syncthreads();                                     // #2: dW2 operands consumed
-    STAMP(7);
-#pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      store_act_fm<LD>(bufB, RT * w + t, h2[t]);
-#pragma unroll
-      for (int s = 0; s < 12; ++s) bufA[(4 * s + q) * LD + row_l[t]] = cur.x[t][s];
-    }
-    __syncthreads();                                     // #3: X, dZ1 visible
-    STAMP(8);
-    // ---- prefetch: the records of step + 1 land in stg (LDS-DMA) while the dW1 tiles, the
-    //      norm exchange and Adam run; every lane has read its rows of this step (sync #1).
-    //      The row split issues them with its partner exchange instead, behind the first
-    //      poll's loads: vmcnt retires in order, so the exchange loads would otherwise wait
-    //      for the gathers.
-#ifndef DDRL_ABL_NO_PREFETCH
-    if (KSP == 1 && step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, idxb, stg, U.R, ub.lds_bytes);
-#endif
-    // the exchange lane (wave NW-1, which issued no gathers) polls the partner's granule
-    // early: when the other branch is ahead, its norm^2 is already there at the exchange
-    const int xlane = 64 * (NW - 1);
-    unsigned long long* const xmine = ub.xchg + (((size_t)p * 2 + (POL ? 0 : 1)) * KSP + kq) * 2 + (step & 1);
-    unsigned long long* const xother = ub.xchg + (((size_t)p * 2 + (POL ? 1 : 0)) * KSP + kq) * 2 + (step & 1);
-    unsigned long long xv = 0;
-    if (tid == xlane) xv = xchg_load(xother);
-    STAMP(9);
-    {
-      // dW1 tiles of this wave: the valid slots are a prefix (tiles w + NW i < 4 nf1)
-#pragma unroll
-      for (int i = NS1; i < NTS; ++i) gt[i] = splat4(0.f);
-      int n1 = 0;
-#pragma unroll
-      for (int i = NS1; i < NTS; ++i) n1 += tv[i] ? 1 : 0;
-#ifdef DDRL_ABL_NO_DW1
-      n1 = -1;
-#endif
-      if (n1 == NS2) dw_tiles_fm<ROWS, NS2>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
-      else if constexpr (NS2 >= 3) {
-        if (n1 == 2) dw_tiles_fm<ROWS, 2>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
-        else if (n1 == 1) dw_tiles_fm<ROWS, 1>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
-      } else if (n1 == 1) dw_tiles_fm<ROWS, 1>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
-    }
-    STAMP(10);
-    if constexpr (KSP == 2) {
-      // last share out, then the partner's: value = mine + partner's (commutative, so
-      // both workgroups hold the same bits)
-#pragma unroll
-      for (int i = NS1; i < NTS; ++i) {
-        gx_put(gx_mine, NP0 + 2 * i, gt[i][0], gt[i][1], gtag, coh);
-        gx_put(gx_mine, NP0 + 2 * i + 1, gt[i][2], gt[i][3], gtag, coh);
-      }
-      float o[2 * NP];
-#ifndef DDRL_ABL_NO_PREFETCH
-      // the next step's record gathers go out right behind the first poll's loads (which
-      // retire first: vmcnt is in order; a re-poll then waits for them too): 13.0 -> 12.9 us
-      // per step against issuing them after the exchange
-      gx_get<NP>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), gtag, o, ub.err, [&] {
-        if (step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, idxb, stg, U.R, ub.lds_bytes);
-      });
-#else
-      gx_get<NP>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), gtag, o, ub.err, [] {});
-#endif
-#pragma unroll
-      for (int k = 0; k < NSLOT; ++k) gs[k] += o[k];
-      if (tid < NSTAT) red[96 + tid] = st_own + o[NSLOT];
-#pragma unroll
-      for (int i = 0; i < NTS; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) gt[i][r] += o[2 * NP0 + 4 * i + r];
-      STAMP(14);
-    } else {
-#pragma unroll
-      for (int k = 0; k < NSLOT; ++k) {
-        const int e = tid + NT * k;
-        float sm = 0.f;
-        if (e < nsb)
-          for (int i = 0; i < NW; ++i) sm += Pb[i * NSB + e];
-        gs[k] = sm;
-      }
-    }
-    float ss = 0.f;
-#pragma unroll
-    for (int k = 0; k < NSLOT; ++k) ss += gs[k] * gs[k];
-#pragma unroll
-    for (int i = 0; i < NTS; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int f = 16 * tfa[i] + 4 * q + r;
-        if (tv[i] && (i < NS1 || f < d)) ss += gt[i][r] * gt[i][r];
-      }
-
-    if (U.grad_out) {   // data-parallel mode: export the raw gradient of this branch
-#pragma unroll
-      for (int i = 0; i < NTS; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int f = 16 * tfa[i] + 4 * q + r, o = 16 * tfo[i] + c;
-          if (tv[i] && (i < NS1 || f < d)) U.grad_out[(i < NS1 ? bo.w2 : bo.w1) + f * 64 + o] = gt[i][r];
-        }
-#pragma unroll
-      for (int k = 0; k < NSLOT; ++k) {
-        const int e = tid + NT * k;
-        if (e < nsb) {
-          int pidx; float* lp;
-          small_param<OB>(e, bo, W, pidx, lp);
-          U.grad_out[pidx] = gs[k];
-        }
-      }
-      if (U.stats && tid == 64) write_stats<POL, NSTAT, NW, KSP>(U.stats + (size_t)step * 8, red, (float)ub.nrows);
-      return;
-    }
-
-    // ---- global norm: local reduction, then swap with the other branch's workgroup ----
-    ss = wave_sum(ss);
-    if (lane == 0) red[64 + w] = ss;
-    __syncthreads();                                     // #4
-    if (tid == xlane) {
-      float local = 0.f;
-      for (int i = 0; i < NW; ++i) local += red[64 + i];
-      const unsigned tag = xchg_tag(ub.epoch, step);
-      xchg_store(xmine, ((unsigned long long)tag << 32) | __float_as_uint(local), coh);
-      unsigned long long v = xv;
-      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-#ifdef DDRL_ABL_NO_EXCHANGE
-      v = ((unsigned long long)tag << 32) | __float_as_uint(local);
-#endif
-      while ((unsigned)(v >> 32) != tag) {
-        v = xchg_load(xother);
-        if ((unsigned)(v >> 32) == tag) break;
-        if (xchg_abandon(t0, ub.err)) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-      const float partner = __uint_as_float((unsigned)(v & 0xffffffffu));
-      const float tot = local + partner;                 // same sum on both workgroups
-      const float gn = sqrtf(tot);
-      red[80] = gn;
-      red[81] = H.grad_clip * fminf(1.f / gn, 1.f / H.grad_clip);
-    }
-    __syncthreads();                                     // #5
-    STAMP(11);
-    if (U.stats && tid == 64 && kq == 0) {   // off the critical path: wave 1, after the exchange
-      write_stats<POL, NSTAT, NW, KSP>(U.stats + (size_t)step * 8, red, (float)ub.nrows);
-      gst(U.stats + (size_t)step * 8 + 6, red[80]);
-      gst(U.stats + (size_t)step * 8 + 7, red[81]);
-    }
-    const float scale = red[81];
-    const float alpha = H.lr * sqrtf(1.f - b2p) / (1.f - b1p);
-    const float c1 = 1.f - H.b1, c2 = 1.f - H.b2;
-
-#ifndef DDRL_ABL_NO_ADAM
-    // ---- tf1 Adam on owned parameters (m, v in registers, weights in LDS) ----
-    // element (f = 16 fa + 4q + r, o = 16 fo + c) sits at ebase[r] + 1024 fa in W1 / W2.
-    // All owned weights are read first, then updated, then written (no read-after-write
-    // ordering between different parameters' LDS words).
-    {
-      float th[NTS][4], ts[NSLOT];
-#pragma unroll
-      for (int i = 0; i < NTS; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          th[i][r] = (i < NS1 ? W.w2 : W.w1)[ebase[r] + 1024 * tfa[i]];
-#pragma unroll
-      for (int k = 0; k < NSLOT; ++k) {
-        const int e = tid + NT * k;
-        ts[k] = 0.f;
-        if (e < nsb) { int pidx; float* lp; small_param<OB>(e, bo, W, pidx, lp); ts[k] = *lp; }
-      }
-#pragma unroll
-      for (int i = 0; i < NTS; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float g = gt[i][r] * scale;
-          mt[i][r] = mt[i][r] + (g - mt[i][r]) * c1;
-          vt4[i][r] = vt4[i][r] + (g * g - vt4[i][r]) * c2;
-          th[i][r] = th[i][r] - (mt[i][r] * alpha) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vt4[i][r]) + H.eps);
-        }
-
-#pragma unroll
-      for (int k = 0; k < NSLOT; ++k) {
-        const float g = gs[k] * scale;
-        ms[k] = ms[k] + (g - ms[k]) * c1;
-        vs[k] = vs[k] + (g * g - vs[k]) * c2;
-        ts[k] = ts[k] - (ms[k] * alpha) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vs[k]) + H.eps);
-      }
-#pragma unroll
-      for (int i = 0; i < NTS; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int f = 16 * tfa[i] + 4 * q + r;
-          if (tv[i] && (i < NS1 || f < d))
-            (i < NS1 ? W.w2 : W.w1)[ebase[r] + 1024 * tfa[i]] = th[i][r];
-        }
-#pragma unroll
-      for (int k = 0; k < NSLOT; ++k) {
-        const int e = tid + NT * k;
-        if (e < nsb) { int pidx; float* lp; small_param<OB>(e, bo, W, pidx, lp); *lp = ts[k]; }
-      }
-    }
-#endif
-    b1p = b1p * H.b1;
-    b2p = b2p * H.b2;
-    STAMP(12);
-    wait_vmcnt0();                                       // this wave's record gathers landed
-    if (tid < ROWS) idxb[tid] = nxt;                     // row indices of step + 2
-    __syncthreads();                                     // #6: weights updated, stg / idxb ready
-    if (tid < ROWS) nxt = step + 3 < last && gok ? row_index(U, step + 3, gr, true) : 0;
-    STAMP(13);
-  }
-  STAMP_DONE;
-  if (U.grad_out || kq != 0) return;   // the row halves hold identical state: one writes it back
-
-  // ---- write back weights, optimizer state, beta powers ----
-#pragma unroll
-  for (int i = 0; i < NTS; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int f = 16 * tfa[i] + 4 * q + r, o = 16 * tfo[i] + c;
-      if (!(tv[i] && (i < NS1 || f < d))) continue;
-      const int pidx = (i < NS1 ? bo.w2 : bo.w1) + f * 64 + o;
-      U.m[pidx] = mt[i][r];
-      U.v[pidx] = vt4[i][r];
-    }
-#pragma unroll
-  for (int k = 0; k < NSLOT; ++k) {
-    const int e = tid + NT * k;
-    if (e >= nsb) continue;
-    int pidx; float* lp;
-    small_param<OB>(e, bo, W, pidx, lp);
-    U.m[pidx] = ms[k];
-    U.v[pidx] = vs[k];
-    U.theta[pidx] = *lp;
-  }
-  for (int i = tid; i < 48 * 64; i += NT) {
-    const int f = i >> 6;
-    if (f < d) U.theta[bo.w1 + i] = W.w1[sidx(f, i & 63)];
-  }
-  for (int i = tid; i < 64 * 64; i += NT) U.theta[bo.w2 + i] = W.w2[sidx(i >> 6, i & 63)];
-  if (POL && tid == 0) {
-    U.beta_pow[0] = b1p;
-    U.beta_pow[1] = b2p;
-  }
-}
-
-template <int A, int KS1, int KSP, bool CUP>
-__global__ void __launch_bounds__(64 * waves_for(A, KSP)) k_update_ffn(UpdateBatch ub) {
-  extern __shared__ float lds[];
-  constexpr int NW = waves_for(A, KSP);
-  // block b = p + 8 j, j = KSP branch + kq (branch 0 = policy, kq = row half): the blocks of
-  // one policy are dealt to the same XCD (b mod 8), so its per-step exchanges stay inside
-  // one XCD (speed only; they are agent-scope either way).  Blocks with p >= P have no work.
-  const int p = blockIdx.x & 7;
-  if (p >= ub.h.P) return;
-  const int j = blockIdx.x >> 3, branch = j / KSP, kq = j - branch * KSP;
-  const UpdateArgs U = ub.a[p];
-  if (branch) update_loop<A, KS1, 1, false, NW, KSP, false>(U, ub, lds, p, kq);
-  else update_loop<A, KS1, 2 * A, true, NW, KSP, CUP>(U, ub, lds, p, kq);
-}
-
-// stride: the widest record stride of the launched policies (staging buffer rows)
-static size_t update_lds_bytes(int O, int stride, int ksp) {
-  const int nsb = 64 * O + O + 128 + ncup_slots(O, true);
-  const int nw = waves_for(O / 2, ksp);
-  return (size_t)(BRANCH_LDS_FLOATS + 2 * 64 * (DDRL_MB / ksp + 8) + nw * nsb + 256 +
-                  (DDRL_MB / ksp) * 4 * stg_chunks(stride, O / 2)) * 4;
-}
-
-template <int A, int KS1, bool CUP = false>
-static void launch_update_t(hipStream_t s, UpdateBatch& ub, int P, int stride, int ksp) {
-  ub.lds_bytes = (unsigned)update_lds_bytes(2 * A, stride, ksp);
-  if (ksp == 2)
-    hipLaunchKernelGGL((k_update_ffn<A, KS1, 2, CUP>), dim3(24 + P), dim3(64 * waves_for(A, 2)), ub.lds_bytes, s, ub);
-  else
-    hipLaunchKernelGGL((k_update_ffn<A, KS1, 1, CUP>), dim3(8 + P), dim3(64 * waves_for(A, 1)), ub.lds_bytes, s, ub);
-}
-
-void launch_update_ffn(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n,
-                       int A, int d, int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp,
-                       int* err, unsigned* epoch_ctr) {
-  UpdateBatch ub;
-  for (int p = 0; p < DDRL_MAXP; ++p) ub.a[p] = p < h.P ? ua[p] : UpdateArgs{};
-  ub.h = h;
-  ub.nrows = nrows;
-  ub.inv_n = inv_n;
-  ub.xchg = xchg;
-  ub.gx = gx;
-  ub.err = err;
-  // Every granule tag carries the launch epoch (12 bits, per context). Granules are cleared
-  // only when the epoch wraps: between two clears every launch's epoch is larger than that
-  // of any granule left in the buffers, so a stale granule can never match.  (A memset per
-  // launch costs a fill kernel and a boundary, ~5 us, per data-parallel step.)
-  ub.epoch = (*epoch_ctr)++ % 4095u + 1u;
-  if (ub.epoch == 1) {
-    (void)hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * 8 * DDRL_MAXP, s);
-    (void)hipMemsetAsync(gx, 0, gx_bytes(DDRL_MAXP), s);
-  }
-  if (cup)   // "cup": one shared leg policy, A = 2, d <= 20 (capi validate)
-    launch_update_t<2, 5, true>(s, ub, h.P, stride, ksp);
-  else
-    DDRL_DISPATCH_A_KS1(A, d, launch_update_t, s, ub, h.P, stride, ksp);
-}
 
 size_t gx_bytes(int P) { return sizeof(unsigned long long) * (size_t)P * 2 * 2 * 2 * GX_MAX_PAIRS * 256 * 2; }
 
@@ -1085,9 +40,11 @@ size_t gx_bytes(int P) { return sizeof(unsigned long long) * (size_t)P * 2 * 2 *
 template <int K>
 __global__ void __launch_bounds__(1024) k_apply_adam(const float* __restrict__ grad, int n,
                                                      float* theta, float* m, float* v,
-                                                     float* beta_pow, UpdateHyper h, float gscale, int xcd) {
+                                                     float* beta_pow, UpdateHyper h, float gscale, int xcd,
+                                                     const int* err) {
   __shared__ float red[16];
   if (K > 0 && (int)(blockIdx.x & 7) != xcd) return;   // not on the policy's XCD
+  if (*err) return;   // the step's gradient launch failed: leave the weights (the host restores them)
   const int tid = threadIdx.x;
   const float b1p = beta_pow[0], b2p = beta_pow[1];
   const int i0 = K > 0 ? (int)(blockIdx.x >> 3) * 1024 + tid : tid;
@@ -1169,15 +126,15 @@ __global__ void __launch_bounds__(1024) k_apply_adam(const float* __restrict__ g
 }
 
 void launch_apply_adam(hipStream_t s, const float* grad, int n, float* theta, float* m, float* v,
-                       float* beta_pow, const UpdateHyper& h, float gscale, int xcd) {
+                       float* beta_pow, const UpdateHyper& h, float gscale, int xcd, const int* err) {
   const int k = (n + 1023) / 1024;
   xcd &= 7;
   if (k <= 16)        // fcnet policies: 11,205 .. 15,057 parameters
     hipLaunchKernelGGL(k_apply_adam<16>, dim3(8 * k), dim3(1024), 0, s, grad, n, theta, m, v, beta_pow, h, gscale,
-                       xcd);
+                       xcd, err);
   else if (k <= 32)   // GraphNet: 28,869 parameters
     hipLaunchKernelGGL(k_apply_adam<32>, dim3(8 * k), dim3(1024), 0, s, grad, n, theta, m, v, beta_pow, h, gscale,
-                       xcd);
+                       xcd, err);
   else
-    hipLaunchKernelGGL(k_apply_adam<0>, dim3(1), dim3(1024), 0, s, grad, n, theta, m, v, beta_pow, h, gscale, 0);
+    hipLaunchKernelGGL(k_apply_adam<0>, dim3(1), dim3(1024), 0, s, grad, n, theta, m, v, beta_pow, h, gscale, 0, err);
 }

@@ -291,6 +291,20 @@ class Context:
         _ck(self.lib.ddrl_records_get(self.h, pid, a.ctypes.data, a.size))
         return a
 
+    def records_tensor(self, pid):
+        """The policy's device record buffer [T * C][stride] as a torch tensor (no copy: a
+        view over ddrl_device_buffers' pointer through __cuda_array_interface__)."""
+        import torch
+        rec, lv, par, an = VP(), VP(), VP(), VP()
+        _ck(self.lib.ddrl_device_buffers(self.h, pid, C.byref(rec), C.byref(lv), C.byref(par), C.byref(an)))
+        lay = self.layout[pid]
+        shape = (self.cfg.frag_len * lay["C"], lay["stride"])
+
+        class _View:
+            __cuda_array_interface__ = {"shape": shape, "typestr": "<f4", "data": (rec.value, False),
+                                        "version": 3, "strides": None}
+        return torch.as_tensor(_View(), device=torch.device("cuda", self.device))
+
     def records_set(self, pid, rec):
         a = np.ascontiguousarray(rec, np.float32)
         _ck(self.lib.ddrl_records_set(self.h, pid, a.ctypes.data, a.size))

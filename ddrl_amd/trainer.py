@@ -61,7 +61,11 @@ class PPOTrainer:
         """Multi-process use: initialize torch.distributed first (one process per GPU).
         Shared-policy envs then train data-parallel (config "parallel": "ddp", the default
         for one policy; "ddp_mode": "split" | "local", see ddrl_amd.ddp); multi-policy envs
-        run as independent replicas ("parallel": "replicas")."""
+        run as independent replicas ("parallel": "replicas").  "parallel": "gather" (any env):
+        every rank rolls out its own envs, the records of all ranks are all-gathered once per
+        iteration into a learner context sized for the union batch, and every rank runs the
+        same fused update over it with the same schedule -- weights identical on all ranks, no
+        per-step collective (the union batch equals a single-process run over all envs)."""
         import torch
         import torch.distributed as dist
         self.torch = torch
@@ -103,6 +107,21 @@ class PPOTrainer:
         self.timesteps_total = 0
         self.iteration = 0
         self.parallel = c.get("parallel") or ("ddp" if self.world > 1 and P == 1 else "replicas")
+        if self.parallel not in ("ddp", "replicas", "gather"):
+            raise ValueError(f"parallel {self.parallel!r}: 'ddp', 'replicas' or 'gather'")
+        self.rctx = self.ctx   # the rollout context (the learner's own, except in "gather" mode)
+        if self.parallel == "gather":
+            from .ddp import Comm
+            self.comm = Comm(self.device if self.world > 1 and dist.get_backend() == "nccl" else "cpu") \
+                if self.world > 1 else None
+            ucfg, _ = make_cfg(env, self.n_envs * self.world, self.T, c)
+            self.ctx = N.Context(ucfg, device, self.stream.cuda_stream)   # learner: union batch
+            for p in range(P):
+                self.ctx.params_set(p, self.rctx.params_get(p))
+            self.pfilter_base = ([self.rctx.policy_filter_get(p) for p in range(P)]
+                                 if self.cfg.policy_filter else None)
+            self.rctx.policy_filter_delta_reset()
+            self.sched_rng = np.random.default_rng(seed + 7919)   # the same schedule on every rank
         if self.parallel == "ddp":
             from .ddp import Comm, DataParallelLearner, HipBackend, NativeDataParallelLearner, native_comm_init
             rccl = dist.get_backend() == "nccl"
@@ -120,20 +139,35 @@ class PPOTrainer:
                                  if self.cfg.policy_filter else None)
             self.ctx.policy_filter_delta_reset()
             self.grad = torch.zeros(self.ctx.n_params[0], dtype=torch.float32, device=self.device)
-        self.ctx.observe(self.backend.reset())
+        self.rctx.observe(self.backend.reset())
 
     # -- one iteration ---------------------------------------------------------------
     def _sample(self):
         torch, cfg = self.torch, self.cfg
+        rctx = self.rctx
         for t in range(self.T):
             eps = torch.randn((self.n_envs, cfg.n_agents, cfg.act_dim), device=self.device,
                               generator=self.noise_gen)
-            self.ctx.act(t, eps, self.actions)
+            rctx.act(t, eps, self.actions)
             obs, fw, cfrc, done = self.backend.step(self.actions)
-            self.ctx.reward(t, fw, cfrc, self.actions, done)
-            self.ctx.observe(obs)
-        self.ctx.bootstrap()
-        self.ctx.gae()
+            rctx.reward(t, fw, cfrc, self.actions, done)
+            rctx.observe(obs)
+        rctx.bootstrap()
+        rctx.gae()
+        if self.parallel == "gather":
+            from .ddp import sync_filters, sync_standardize, standardize_constants
+            for p in range(self.cfg.n_policies):
+                if self.pfilter_base is not None:   # RLlib synchronize_filters
+                    d = rctx.policy_filter_get(p, delta=True)
+                    self.pfilter_base[p] = (sync_filters(self.comm, self.pfilter_base[p], d) if self.comm else
+                                            sync_filters_local(self.pfilter_base[p], d))
+                    rctx.policy_filter_set(p, *self.pfilter_base[p])
+                    self.ctx.policy_filter_set(p, *self.pfilter_base[p])
+                sums = rctx.adv_sums_get(p)
+                norm = sync_standardize(self.comm, sums) if self.comm else standardize_constants(sums)
+                self.ctx.adv_norm_set(p, *norm)
+            rctx.policy_filter_delta_reset()
+            return
         if self.parallel == "ddp":
             from .ddp import sync_filters, sync_standardize
             # The env-side MeanStdFilter is a per-process singleton in the reference
@@ -179,9 +213,27 @@ class PPOTrainer:
         self.kl_coeff[0] = update_kl(self.kl_coeff[0], kl, self.config["kl_target"])
         return learner
 
+    def _gather_records(self):
+        """All-gather every rank's records (rank-major) into the learner context's union batch."""
+        torch = self.torch
+        for p in range(self.cfg.n_policies):
+            src = self.rctx.records_tensor(p)
+            dst = self.ctx.records_tensor(p)
+            if self.world == 1:
+                dst.copy_(src)
+                continue
+            if self.comm.device == "cpu":   # gloo
+                parts = [torch.empty_like(src, device="cpu") for _ in range(self.world)]
+                self.comm.dist.all_gather(parts, src.cpu(), group=self.comm.group)
+                dst.copy_(torch.cat(parts).to(dst.device))
+            else:                           # RCCL: straight into the learner's record buffer
+                self.comm.dist.all_gather_into_tensor(dst, src, group=self.comm.group)
+
     def _learn(self):
         if self.parallel == "ddp":
             return self._learn_ddp()
+        if self.parallel == "gather":
+            self._gather_records()
         torch = self.torch
         P = self.cfg.n_policies
         sh, pe, nbs = [], [], []
@@ -201,6 +253,9 @@ class PPOTrainer:
                             "kl": last[3], "entropy": last[4], "vf_explained_var": last[5],
                             "grad_gnorm": last[6], "entropy_coeff": self.cfg.entropy_coeff}
             self.kl_coeff[p] = update_kl(self.kl_coeff[p], last[3], self.config["kl_target"])
+        if self.parallel == "gather":   # the next rollout uses the updated weights
+            for p in range(P):
+                self.rctx.params_set(p, self.ctx.params_get(p))
         return learner
 
     def train(self):
@@ -246,7 +301,7 @@ class PPOTrainer:
             arrs[f"{pid}/adam_m"], arrs[f"{pid}/adam_v"] = m, v
             arrs[f"{pid}/beta_powers"] = np.array([b1, b2], np.float32)
             arrs[f"{pid}/kl_coeff"] = np.array([self.kl_coeff[p]])
-        n, M, S = self.ctx.filter_get()
+        n, M, S = self.rctx.filter_get()   # the env-side filter lives where the rollout runs
         arrs["filter/n"], arrs["filter/M"], arrs["filter/S"] = np.array([n]), M, S
         if self.cfg.policy_filter:
             for p, pid in enumerate(self.policy_ids):
@@ -261,14 +316,17 @@ class PPOTrainer:
         z = np.load(path, allow_pickle=False)
         for p, pid in enumerate(self.policy_ids):
             self.ctx.params_set(p, z[f"{pid}/weights"])
+            if self.rctx is not self.ctx:
+                self.rctx.params_set(p, z[f"{pid}/weights"])
             b = z[f"{pid}/beta_powers"]
             self.ctx.adam_set(p, z[f"{pid}/adam_m"], z[f"{pid}/adam_v"], float(b[0]), float(b[1]))
             self.kl_coeff[p] = float(z[f"{pid}/kl_coeff"][0])
-        self.ctx.filter_set(float(z["filter/n"][0]), z["filter/M"], z["filter/S"])
+        self.rctx.filter_set(float(z["filter/n"][0]), z["filter/M"], z["filter/S"])
         if self.cfg.policy_filter:
             for p, pid in enumerate(self.policy_ids):
-                self.ctx.policy_filter_set(p, float(z[f"{pid}/filter/n"][0]), z[f"{pid}/filter/M"],
-                                           z[f"{pid}/filter/S"])
+                for cx in {id(self.ctx): self.ctx, id(self.rctx): self.rctx}.values():
+                    cx.policy_filter_set(p, float(z[f"{pid}/filter/n"][0]), z[f"{pid}/filter/M"],
+                                         z[f"{pid}/filter/S"])
         meta = json.loads(bytes(z["meta"]).decode())
         self.iteration, self.timesteps_total = meta["iteration"], meta["timesteps_total"]
 
@@ -342,14 +400,29 @@ class PPOTrainer:
             self.ctx.adam_set(p, st["adam_m"], st["adam_v"], *st["beta_powers"])
             if self.cfg.policy_filter and st["filter"] is not None:
                 self.ctx.policy_filter_set(p, *st["filter"])
+                self.rctx.policy_filter_set(p, *st["filter"])
+            if self.rctx is not self.ctx:
+                self.rctx.params_set(p, st["weights"])
             if st["kl_coeff"] is not None:
-                self.kl_coeff[p] = st["kl_coeff"]
-        if self.parallel == "ddp" and self.pfilter_base is not None:
+                # the file's cur_kl_coeff is the coefficient the checkpointed iteration trained
+                # with; the next iteration's is update_kl of it and that iteration's kl (RLlib
+                # runs update_kl after the learner step, ppo.py UpdateKL)
+                kl = (st.get("learner_stats") or {}).get("kl")
+                self.kl_coeff[p] = (update_kl(st["kl_coeff"], kl, self.config["kl_target"]) if kl is not None
+                                    else st["kl_coeff"])
+        if self.parallel in ("ddp", "gather") and self.pfilter_base is not None:
             self.pfilter_base = [self.ctx.policy_filter_get(p) for p in range(self.cfg.n_policies)]
         return list(self.policy_ids)
 
     def stop(self):
+        if self.rctx is not self.ctx:
+            self.rctx.close()
         self.ctx.close()
+
+
+def sync_filters_local(base, delta):
+    from .ddp import merge_running_stats
+    return merge_running_stats(base, [delta])
 
 
 def update_kl(kl_coeff, sampled_kl, kl_target=0.01):

@@ -676,11 +676,13 @@ def update_kl(kl_coeff, sampled_kl, kl_target=0.01):
     return kl_coeff
 
 
-def ppo_update(model, params, shapes, adam, batch, shuffle, perms, kl_coeff, cfg, steps=None, snapshots=None):
+def ppo_update(model, params, shapes, adam, batch, shuffle, perms, kl_coeff, cfg, steps=None, snapshots=None,
+               gradlog=None):
     """Runs the minibatch loop for one policy.  `model` is "ffn", "cup" or "gnn".  `batch` is
     a dict of row arrays: obs (+ leg for "cup"; X/node_idx for "gnn"), actions, logits, logp, vf_preds, adv
     (already standardized) and vt.  Returns (params, per-step stats list).  `snapshots`: an
-    optional dict {step count: None} filled with the flat parameters after that many steps."""
+    optional dict {step count: None} filled with the flat parameters after that many steps;
+    `gradlog`: an optional list that receives each step's clipped flat gradient (Adam's input)."""
     mb = cfg.get("sgd_minibatch_size", 128)
     epochs, nb = perms.shape
     theta = pack(params, shapes)
@@ -709,6 +711,8 @@ def ppo_update(model, params, shapes, adam, batch, shuffle, perms, kl_coeff, cfg
             glist = [g[n] for n, _ in shapes]
             clipped, gn = clip_by_global_norm(glist, cfg.get("grad_clip", 0.5))
             flat = np.concatenate([c.reshape(-1) for c in clipped])
+            if gradlog is not None:
+                gradlog.append(flat.copy())
             theta = adam.apply(theta, flat)
             st["grad_gnorm"] = float(gn)
             out_stats.append(st)

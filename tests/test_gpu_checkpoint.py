@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 from oracle import ddrl_oracle as O
-from tests.gpu_harness import make_ctx, run_rollout
+from tests.gpu_harness import make_ctx, run_rollout, strict_params_check
 
 pytestmark = pytest.mark.gpu
 FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ckpt_local_1250.npz")
@@ -45,6 +45,8 @@ def test_published_local_policies_rollout_and_update():
         a.m, a.v = z[f"{name}/adam_m"].copy(), z[f"{name}/adam_v"].copy()
         a.b1p, a.b2p = np.float32(b1p), np.float32(b2p)
         adams.append(a)
+    import copy
+    adam0 = copy.deepcopy(adams)      # the published optimizer state, before the oracle steps it
     np.testing.assert_array_equal(ctx.params_get(0), z[f"{names[0]}/weights"])   # round trip
     rng = np.random.default_rng(23)
     filt = (1000.0, rng.normal(size=43) * 0.3, np.abs(rng.normal(size=43)) * 999.0 + 10.0)
@@ -86,6 +88,8 @@ def test_published_local_policies_rollout_and_update():
         diff = np.abs(ctx.params_get(p) - want)
         assert np.mean(diff <= 1e-5 + 1e-5 * np.abs(want)) >= 0.999, diff.max()
         assert diff.max() <= 2 * cfg.lr * steps + 1e-5
+        strict_params_check(ctx.params_get(p), "ffn", params[p], shapes, batch, sh_l[p], pe_l[p], kls[p], steps,
+                            adam=adam0[p], lr=float(adam0[p].lr), msg=f"published {names[p]}")
         m, v, b1p, b2p = ctx.adam_get(p)
         _close(m, adams[p].m, rtol=1e-4, atol=1e-7, msg="Adam m")
         assert b1p == np.float32(adams[p].b1p) and b2p == np.float32(adams[p].b2p)

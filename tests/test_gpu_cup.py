@@ -12,7 +12,8 @@ import numpy as np
 import pytest
 
 from oracle import ddrl_oracle as O
-from tests.gpu_harness import CUP_CONFIG, CUP_ENV, CupOracleRollout, init_cup_params, make_ctx, run_rollout
+from tests.gpu_harness import (CUP_CONFIG, CUP_ENV, CupOracleRollout, init_cup_params, make_ctx, run_rollout,
+                                strict_params_check)
 
 pytestmark = pytest.mark.gpu
 
@@ -106,6 +107,8 @@ def test_cup_fused_update_parity(steps):
     diff = np.abs(got - want)
     assert np.mean(diff <= 1e-5 + 1e-5 * np.abs(want)) >= 0.999, diff.max()
     assert diff.max() <= 2 * cfg.lr * steps + 1e-5
+    strict_params_check(got, "cup", params[0], shapes, _batch(ref, lay, 19, 2, norms[0]), sh, pe, 0.25, steps,
+                        lr=cfg.lr, msg="cup")
     # the coupling table itself moved, and matches
     np.testing.assert_allclose(got[-8:], want[-8:], rtol=1e-5, atol=1e-5)
     assert np.abs(got[-8:] - O.pack(params[0], shapes)[-8:]).max() > 0

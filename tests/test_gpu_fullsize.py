@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 from oracle import ddrl_oracle as O
-from tests.gpu_harness import init_params, make_ctx
+from tests.gpu_harness import init_params, make_ctx, strict_params_check
 
 pytestmark = pytest.mark.gpu
 N_ENVS, T = 4096, 200
@@ -111,6 +111,7 @@ def test_fullsize_first_step_and_stability(full):
     diff = np.abs(got - want)
     assert np.mean(diff <= 1e-5 + 1e-5 * np.abs(want)) >= 0.999, diff.max()
     assert diff.max() <= 2 * cfg.lr + 1e-5
+    strict_params_check(got, "ffn", params[0], shapes, batch, sh.numpy(), pe.numpy(), 0.2, 1, msg="full size")
     # 200 further steps (a new launch runs the schedule from its first minibatch again)
     ctx.ppo_update(1, [sh.cuda(), None, None, None], [pe.cuda(), None, None, None], [0.2] * 4, max_steps=200)
     ctx.synchronize()

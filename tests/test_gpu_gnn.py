@@ -8,7 +8,8 @@ import numpy as np
 import pytest
 
 from oracle import ddrl_oracle as O
-from tests.gpu_harness import GNN_ENV, GnnOracleRollout, init_gnn_params, make_ctx, run_rollout
+from tests.gpu_harness import (GNN_ENV, GnnOracleRollout, init_gnn_params, make_ctx, run_rollout,
+                                strict_params_check)
 
 pytestmark = pytest.mark.gpu
 SHAPES = O.gnn_param_shapes(4)
@@ -123,6 +124,10 @@ def test_gnn_grad_and_apply():
     got = ctx.params_get(0)
     diff = np.abs(got - ref)
     assert np.mean(diff <= 1e-5 + 1e-5 * np.abs(ref)) >= 0.999 and diff.max() <= 2 * 3e-4 + 1e-5
+    rest = np.setdiff1d(np.arange(rec.shape[0], dtype=np.int32), rows)
+    sh1 = np.concatenate([rows, rest]).astype(np.int32)
+    strict_params_check(got, "gnn", params, SHAPES, b, sh1, np.arange(sh1.size // 128, dtype=np.int32)[None],
+                        0.2, 1, msg="gnn apply")
     ctx.close()
 
 
@@ -146,6 +151,8 @@ def test_gnn_update_parity():
     diff = np.abs(got - ref)
     frac = np.mean(diff <= 1e-5 + 1e-5 * np.abs(ref))
     assert frac >= 0.999 and diff.max() <= 2 * cfg.lr * steps + 1e-5, (frac, diff.max())
+    strict_params_check(got, "gnn", params, SHAPES, _batch(rec, lay, norms[0]), sh, pe, 0.3, steps, lr=cfg.lr,
+                        msg="gnn update")
     m, v, b1p, b2p = ctx.adam_get(0)
     assert b1p == np.float32(adam.b1p) and b2p == np.float32(adam.b2p)
     st = ctx.ppo_stats(0, steps)

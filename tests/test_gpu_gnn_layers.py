@@ -13,7 +13,8 @@ import numpy as np
 import pytest
 
 from oracle import ddrl_oracle as O
-from tests.gpu_harness import GNN_ENV, GnnOracleRollout, init_gnn_params, make_ctx, run_rollout
+from tests.gpu_harness import (GNN_ENV, GnnOracleRollout, init_gnn_params, make_ctx, run_rollout,
+                                strict_params_check)
 
 pytestmark = pytest.mark.gpu
 LAYERS = ["gcn", "mpnn2", "gat1", "mpnn"]
@@ -144,6 +145,8 @@ def test_layer_update_3_steps_and_100_step_drift(layer):
             got, ref = ctx.params_get(0), O.pack(new, shapes)
             diff = np.abs(got - ref)
             assert np.mean(diff <= 1e-5 + 1e-5 * np.abs(ref)) >= 0.999 and diff.max() <= 2 * cfg.lr * steps + 1e-5
+            strict_params_check(got, "gnn", params, shapes, batch, sh, pe, 0.3, steps, lr=cfg.lr,
+                                cfg={"gnn_layer": layer}, msg=layer)
             m, v, b1p, b2p = ctx.adam_get(0)
             assert b1p == np.float32(adam.b1p) and b2p == np.float32(adam.b2p)
             st = ctx.ppo_stats(0, steps)

@@ -15,7 +15,7 @@ import pytest
 
 from ddrl_amd import native as N
 from oracle import ddrl_oracle as O
-from tests.gpu_harness import init_params, make_ctx, run_rollout
+from tests.gpu_harness import init_params, make_ctx, run_rollout, strict_params_check
 
 pytestmark = pytest.mark.gpu
 RT, AT = 1e-5, 1e-5
@@ -203,6 +203,8 @@ def test_ppo_update_parity(env, n, T, steps, config):
                                   np.float32(kls[p]), {"entropy_coeff": 0.0}, steps=steps)
         got = ctx.params_get(p)
         _params_close(got, O.pack(new, shapes), cfg.lr, steps, f"{env} p{p}")
+        strict_params_check(got, "ffn", params[p], shapes, batch, shuffles[p], perms[p], kls[p], steps,
+                            lr=cfg.lr, msg=f"{env} p{p}")
         m, v, b1p, b2p = ctx.adam_get(p)
         assert b1p == np.float32(adam.b1p) and b2p == np.float32(adam.b2p)
         st = ctx.ppo_stats(p, steps)
@@ -237,8 +239,8 @@ def test_full_schedule_runs_and_stays_close():
     new, stats = O.ppo_update("ffn", params[p], shapes, adam, batch, sh, pe, np.float32(0.2), {})
     got = ctx.params_get(p)
     ref = O.pack(new, shapes)
-    diff = np.abs(got - ref)
-    assert np.mean(diff <= 1e-4) >= 0.999 and diff.max() <= 2 * 3e-4 * 20
+    assert np.abs(got - ref).max() <= 1e-5
+    strict_params_check(got, "ffn", params[p], shapes, batch, sh, pe, 0.2, 20, msg="full schedule")
     st = ctx.ppo_stats(p, 20)
     _close(st[-1, 0], stats[-1]["total_loss"], rtol=1e-3, atol=1e-4)
     ctx.close()
@@ -283,6 +285,11 @@ def test_ddp_grad_and_apply_match_fused_step():
     clipped, _ = O.clip_by_global_norm([gref], 0.5)
     ref = adam.apply(O.pack(params[0], shapes), clipped[0])
     _params_close(ctx.params_get(0), ref, 3e-4, 1, "ddp apply")
+    # the same step as a one-step schedule whose first minibatch is `rows`, against fp64
+    rest = np.setdiff1d(np.arange(T * lay["C"], dtype=np.int32), rows)
+    sh1 = np.concatenate([rows, rest]).astype(np.int32)
+    pe1 = np.arange(sh1.size // 128, dtype=np.int32)[None]
+    strict_params_check(ctx.params_get(0), "ffn", params[0], shapes, batch, sh1, pe1, 0.2, 1, msg="ddp apply")
     ctx.close()
 
 

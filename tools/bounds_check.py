@@ -21,7 +21,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 from ddrl_amd import native as N  # noqa: E402
 
-LIB = os.path.join(os.path.dirname(N.LIB_PATH), "libddrl_hip_bounds.so")
+LIB = os.path.join(os.path.dirname(N.LIB_PATH), os.environ.get("DDRL_BOUNDS_LIB", "libddrl_hip_bounds.so"))
 KINDS = ["staging_row", "record_row", "schedule_index", "lds_dma_dst", "staged_read", "param_index"]
 
 
