@@ -13,6 +13,7 @@
 #ifndef DDRL_FFN_AT
 #define DDRL_FFN_AT 0
 #endif
+
 #if DDRL_FFN_AT
 #define DDRL_FFN_LAUNCH launch_update_ffn_atomic
 #else
@@ -32,6 +33,8 @@ namespace {
 // each (one 16-row tile per wave, four waves) and swap their partial gradients every step
 // through tagged 8-byte granules; both then hold the same summed gradient and run the same
 // clip + Adam, so their weight images stay bit-identical.
+typedef float float2v __attribute__((ext_vector_type(2)));
+
 template <int NW, int ROWS>
 struct Geo {
   static constexpr int NT = 64 * NW;
@@ -209,23 +212,37 @@ struct RowData {
 // Issued by waves 0 .. NW-2: the last wave keeps its vector-memory counter free for the
 // norm exchange (an early partner poll would otherwise wait for the gathers too).
 template <int NW, int ROWS>
-__device__ __forceinline__ void issue_rows(const float* rec, int stride, int cpr, int cpr_l, const int* idxb,
-                                           float* stg, int R, unsigned lds_bytes) {
+__device__ __forceinline__ void issue_rows(const float* rec, int stride, int cpr, int cpr_l, float inv_cpr_l,
+                                           const int* idxb, float* stg, int R, unsigned lds_bytes) {
   const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
   if (w == NW - 1) return;
+  // at most 20 chunks per record (fcnet records: d <= 48, A <= 8 -> stride <= 80 floats), so a
+  // wave issues at most MI batches; every staged row index is read from LDS first (one
+  // latency for all batches), then the gathers go out back to back
+  constexpr int MI = (ROWS * 20 + 64 * (NW - 1) - 1) / (64 * (NW - 1));
   const int nchunk = ROWS * cpr_l;
-  const float inv = 1.f / (float)cpr_l;
-  for (int base = 64 * w; base < nchunk; base += 64 * (NW - 1)) {   // wave-uniform
-    const int g = base + lane;
-    int row = (int)(((float)g + 0.5f) * inv);
-    const int k = min(g - row * cpr_l, cpr - 1);
-    const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr(stg + 4 * base));
+  int idx[MI], kk[MI];
+#pragma unroll
+  for (int it = 0; it < MI; ++it) {
+    const int g = 64 * w + 64 * (NW - 1) * it + lane;
+    int row = (int)(((float)g + 0.5f) * inv_cpr_l);
+    kk[it] = min(g - row * cpr_l, cpr - 1);
+    idx[it] = 0;
     if (g < nchunk) {
-      if (!BCHK(row >= 0 && row < ROWS && k >= 0, 0)) row = 0;
-      int idx = idxb[row];
-      if (!BCHK(idx >= 0 && idx < R, 1)) idx = 0;
+      if (!BCHK(row >= 0 && row < ROWS && kk[it] >= 0, 0)) row = 0;
+      idx[it] = idxb[row];
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < MI; ++it) {
+    const int base = 64 * w + 64 * (NW - 1) * it;          // wave-uniform
+    if (base >= nchunk) break;
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lds_addr(stg + 4 * base));
+    if (base + lane < nchunk) {
+      int i = idx[it];
+      if (!BCHK(i >= 0 && i < R, 1)) i = 0;
       if (BCHK(dst + 16u * (unsigned)lane + 16u <= lds_bytes, 3))
-        glds16(rec + (size_t)idx * stride + 4 * k, dst);
+        glds16(rec + (size_t)i * stride + 4 * kk[it], dst);
     }
   }
   (void)R; (void)lds_bytes;
@@ -599,6 +616,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   float* bufD = bufH + 64 * LD;             // HMF: feature-major [16][LD] dout
   float* stg = red + 256 + (HMF ? 80 * LD : 0);   // [ROWS][stride] records of the next step (16 B aligned)
   const int stride = U.lay.stride, cpr = stride >> 2, cpr_l = stg_chunks(stride, A);
+  const float inv_cpr_l = 1.f / (float)cpr_l;
 
   // w is wave-uniform: readfirstlane keeps it (and the tile indices derived from it) in SGPRs
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, q = lane >> 4,
@@ -623,7 +641,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   const bool gok = tid < ROWS && gr < ub.nrows;
   if (tid < ROWS) idxb[tid] = U.step0 < last && gok ? row_index(U, U.step0, gr, true) : 0;
   __syncthreads();
-  if (U.step0 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, idxb, stg, U.R, ub.lds_bytes);
+  if (U.step0 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, inv_cpr_l, idxb, stg, U.R, ub.lds_bytes);
   stage_branch_batched<OB, NT>(U.theta, d, bo, lds, W, NCUP);
   if constexpr (HMF) {
     // the head tile results go to wave 0's partial row; the other waves' dWo partials stay 0
@@ -655,16 +673,22 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     }
   }
   float ms[NSLOT], vs[NSLOT];
+  int sp_pidx[NSLOT], sp_lds[NSLOT];   // loop invariants: parameter index and LDS word of each slot
 #pragma unroll
   for (int k = 0; k < NSLOT; ++k) {
     const int e = tid + NT * k;
     ms[k] = vs[k] = 0.f;
-    if (e < nsb && !U.grad_out) {
+    sp_pidx[k] = sp_lds[k] = 0;
+    if (e < nsb) {
       int pidx; float* lp;
       small_param<OB>(e, bo, W, pidx, lp);
       BCHK(pidx >= 0 && pidx < of.n + NCUP, 5);
-      ms[k] = U.m[pidx];
-      vs[k] = U.v[pidx];
+      sp_pidx[k] = pidx;
+      sp_lds[k] = (int)(lp - lds);
+      if (!U.grad_out) {
+        ms[k] = U.m[pidx];
+        vs[k] = U.v[pidx];
+      }
     }
   }
   int ebase[4];
@@ -902,7 +926,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     //      poll's loads: vmcnt retires in order, so the exchange loads would otherwise wait
     //      for the gathers.
 #ifndef DDRL_ABL_NO_PREFETCH
-    if (KSP == 1 && step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, idxb, stg, U.R, ub.lds_bytes);
+    if (KSP == 1 && step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, inv_cpr_l, idxb, stg, U.R, ub.lds_bytes);
 #endif
     // the exchange lane (wave NW-1, which issued no gathers) polls the partner's granule
     // early: when the other branch is ahead, its norm^2 is already there at the exchange
@@ -943,7 +967,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       // retire first: vmcnt is in order; a re-poll then waits for them too): 13.0 -> 12.9 us
       // per step against issuing them after the exchange
       gx_get<NP>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), gtag, o, ub.err, [&] {
-        if (step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, idxb, stg, U.R, ub.lds_bytes);
+        if (step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, inv_cpr_l, idxb, stg, U.R, ub.lds_bytes);
       });
 #else
       gx_get<NP>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), gtag, o, ub.err, [] {});
@@ -988,11 +1012,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 #pragma unroll
       for (int k = 0; k < NSLOT; ++k) {
         const int e = tid + NT * k;
-        if (e < nsb) {
-          int pidx; float* lp;
-          small_param<OB>(e, bo, W, pidx, lp);
-          U.grad_out[pidx] = gs[k];
-        }
+        if (e < nsb) U.grad_out[sp_pidx[k]] = gs[k];
       }
       if (U.stats && tid == 64) write_stats<POL, NSTAT, NW, KSP>(U.stats + (size_t)step * 8, red, inv_rows);
       return;
@@ -1031,11 +1051,14 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     }
     __syncthreads();                                     // #5
     STAMP(11);
-    if (U.stats && tid == 64 && kq == 0) {   // off the critical path: wave 1, after the exchange
+    auto stats_out = [&] {
       write_stats<POL, NSTAT, NW, KSP>(U.stats + (size_t)step * 8, red, inv_rows);
       gst(U.stats + (size_t)step * 8 + 6, red[80]);
       gst(U.stats + (size_t)step * 8 + 7, red[81]);
-    }
+    };
+    // KSP = 1: wave 1, right after the exchange (the per-wave partials red[w * 8 + k] are
+    // rewritten by the next step's loss); KSP = 2: after sync #6, off every critical path
+    if (KSP == 1 && U.stats && tid == 64 && kq == 0) stats_out();
     const float scale = red[81];
     const float c1 = 1.f - H.b1, c2 = 1.f - H.b2;
 
@@ -1055,16 +1078,28 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       for (int k = 0; k < NSLOT; ++k) {
         const int e = tid + NT * k;
         ts[k] = 0.f;
-        if (e < nsb) { int pidx; float* lp; small_param<OB>(e, bo, W, pidx, lp); ts[k] = *lp; }
+        ts[k] = e < nsb ? lds[sp_lds[k]] : 0.f;
       }
+      // two elements per instruction (v_pk_* ops): the same fused operations, element by
+      // element, as the scalar form g = gt s; m += (gt s - m) c1; v += (g g - v) c2;
+      // theta -= (m alpha) / (sqrt(v) + eps)
 #pragma unroll
       for (int i = 0; i < NTS; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float g = gt[i][r] * scale;
-          mt[i][r] = mt[i][r] + (g - mt[i][r]) * c1;
-          vt4[i][r] = vt4[i][r] + (g * g - vt4[i][r]) * c2;
-          th[i][r] = th[i][r] - (mt[i][r] * alpha) * __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(vt4[i][r]) + H.eps);
+        for (int h = 0; h < 2; ++h) {
+          const float2v gr = {gt[i][2 * h], gt[i][2 * h + 1]};
+          float2v m2 = {mt[i][2 * h], mt[i][2 * h + 1]}, v2 = {vt4[i][2 * h], vt4[i][2 * h + 1]};
+          const float2v sc = {scale, scale}, k1 = {c1, c1}, k2 = {c2, c2}, al = {alpha, alpha};
+          const float2v g = gr * sc;
+          m2 = __builtin_elementwise_fma(__builtin_elementwise_fma(gr, sc, -m2), k1, m2);
+          v2 = __builtin_elementwise_fma(__builtin_elementwise_fma(g, g, -v2), k2, v2);
+          float2v den = {__builtin_amdgcn_sqrtf(v2[0]), __builtin_amdgcn_sqrtf(v2[1])};
+          den = den + (float2v){H.eps, H.eps};
+          const float2v rc = {__builtin_amdgcn_rcpf(den[0]), __builtin_amdgcn_rcpf(den[1])};
+          const float2v t2 = __builtin_elementwise_fma(-(m2 * al), rc, (float2v){th[i][2 * h], th[i][2 * h + 1]});
+          mt[i][2 * h] = m2[0]; mt[i][2 * h + 1] = m2[1];
+          vt4[i][2 * h] = v2[0]; vt4[i][2 * h + 1] = v2[1];
+          th[i][2 * h] = t2[0]; th[i][2 * h + 1] = t2[1];
         }
 
 #pragma unroll
@@ -1085,7 +1120,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 #pragma unroll
       for (int k = 0; k < NSLOT; ++k) {
         const int e = tid + NT * k;
-        if (e < nsb) { int pidx; float* lp; small_param<OB>(e, bo, W, pidx, lp); *lp = ts[k]; }
+        if (e < nsb) lds[sp_lds[k]] = ts[k];
       }
     }
 #endif
@@ -1096,6 +1131,8 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     if (tid < ROWS) idxb[tid] = nxt;                     // row indices of step + 2
     __syncthreads();                                     // #6: weights updated, stg / idxb ready
     if (tid < ROWS) nxt = step + 3 < last && gok ? row_index(U, step + 3, gr, true) : 0;
+    // red[80..81] / red[96..] hold until the next step's exchanges (after its sync #1)
+    if (KSP == 2 && U.stats && tid == 64 && kq == 0) stats_out();
     STAMP(13);
   }
   STAMP_DONE;

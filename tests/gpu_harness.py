@@ -66,9 +66,16 @@ class OracleRollout:
         self.pf = ([O.RunningStat((cfg.obs_dim[p],)) for p in range(cfg.n_policies)]
                    if getattr(cfg, "policy_filter", 0) else None)
 
-    def observe(self, obs):
+    def observe(self, obs, bounds=None):
+        """bounds: env ranges observed by separate calls (ddrl_observe_range), each one filter
+        push + normalization of its own rows; default one call over all envs."""
+        bounds = [0, obs.shape[0]] if bounds is None else bounds
+        parts = [self._observe_block(obs[a:b]) for a, b in zip(bounds[:-1], bounds[1:])]
+        self.stage = [np.concatenate([pp[i] for pp in parts]) for i in range(len(parts[0]))]
+
+    def _observe_block(self, obs):
         normed = O.mean_std_filter(obs, self.rs, update=True, clip=self.cfg.filter_clip)
-        self.stage = []
+        stage = []
         tables = self.model_tables()
         # gather columns; the constants -1 / -2 (LegID one-hot) become 0 / 1
         ext = np.concatenate([normed, np.zeros((normed.shape[0], 1)), np.ones((normed.shape[0], 1))], 1)
@@ -78,7 +85,8 @@ class OracleRollout:
             x = np.stack(cols, 1).reshape(-1, self.cfg.obs_dim[p])   # c = e * k + slot
             if self.pf is not None:
                 x = O.mean_std_filter(x, self.pf[p], update=True, clip=None)
-            self.stage.append(x.astype(np.float32))
+            stage.append(x.astype(np.float32))
+        return stage
 
     def model_tables(self):
         return getattr(self.inst, "policy_obs_indices", self.inst.obs_indices)
@@ -263,11 +271,11 @@ class GnnOracleRollout(OracleRollout):
         self.rec[0]["obs"] = np.zeros((T, N_ * 4, 93), np.float32)
         self.node_tables = [inst.obs_indices[a] for a in self.agents]
 
-    def observe(self, obs):
+    def _observe_block(self, obs):
         normed = O.mean_std_filter(obs, self.rs, update=True, clip=self.cfg.filter_clip)
         X = np.stack([O.graph_observation(obs[e].astype(np.float64), normed[e], self.node_tables)
                       for e in range(obs.shape[0])]).astype(np.float32)
-        self.stage = [X]
+        return [X]
 
     def _forward_all(self):
         X = self.stage[0]

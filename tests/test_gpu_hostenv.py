@@ -59,14 +59,18 @@ def _device_loop(ctx, cfg, env, eps, groups):
     return trace
 
 
-def _oracle_over_trace(cfg, inst, params, filt, trace, eps, gnn):
-    """The oracle rollout over the host env plane's raw outputs (see the module docstring)."""
+def _oracle_over_trace(cfg, inst, params, filt, trace, eps, gnn, groups):
+    """The oracle rollout over the host env plane's raw outputs (see the module docstring).
+    Both HIP paths observe each env group by its own ranged call (one filter push and
+    normalization per group), so the oracle filters group by group too."""
+    n = cfg.n_envs
+    lo = [n * k // groups for k in range(groups + 1)]
     orc = (GnnOracleRollout if gnn else OracleRollout)(cfg, inst, params, filt)
-    orc.observe(trace[0])
+    orc.observe(trace[0], lo)
     for t, (fw, cfrc, done, obs) in enumerate(trace[1:]):
         a = orc.act(t, eps[t])
         orc.reward(t, fw, cfrc, a, done)
-        orc.observe(obs)
+        orc.observe(obs, lo)
     orc.bootstrap()
     return orc, orc.gae()
 
@@ -115,7 +119,7 @@ def test_pipelined_host_rollout_matches_device_loop(env_name, n, T, groups, conf
     np.testing.assert_array_equal(envs[0].obs, envs[1].obs)
     # both against the oracle run on the host env plane's raw outputs
     assert len(trace) == T + 1
-    orc, norms = _oracle_over_trace(cfg, inst, params, filt, trace, eps.cpu().numpy(), gnn)
+    orc, norms = _oracle_over_trace(cfg, inst, params, filt, trace, eps.cpu().numpy(), gnn, groups)
     assert fa[0] == orc.rs.n
     np.testing.assert_allclose(fa[1], orc.rs.M, rtol=1e-12, atol=1e-12)
     np.testing.assert_allclose(fa[2], orc.rs.S, rtol=1e-10, atol=1e-9)

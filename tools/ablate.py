@@ -65,7 +65,14 @@ def one(lib, n):
         ctx.ppo_update(0xF, sh, pe, [0.2] * 4)
         ctx.synchronize()
         best = min(best, time.perf_counter() - t0)
-    print(f"{best / (10 * nb) * 1e6:.2f} us/step")
+    import hashlib
+    h = hashlib.sha256()
+    for p in range(4):
+        h.update(ctx.params_get(p).tobytes())
+        for a in ctx.adam_get(p)[:2]:
+            h.update(np.asarray(a).tobytes())
+    # digest of the trained state: variants that claim bit-identical arithmetic must agree
+    print(f"{best / (10 * nb) * 1e6:.2f} us/step state {h.hexdigest()[:16]}")
 
 
 if __name__ == "__main__":

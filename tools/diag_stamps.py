@@ -7,7 +7,9 @@ from ddrl_amd import build, native as N
 extra = os.environ.get("DDRL_EXTRA_FLAGS", "").split()
 tag = "".join(ch for ch in "".join(extra) if ch.isalnum())[:24]
 # prebuilt (here, on the CPU) when DDRL_STAMPS_LIB names it: python tools/diag_stamps.py --build
-stamps_lib = os.path.join(os.path.dirname(N.LIB_PATH), "libddrl_hip_stamps.so")
+# DDRL_STAMPS_LIB=1: libddrl_hip_stamps.so; any other value: that file name in ddrl_amd/ (variants)
+_sl = os.environ.get("DDRL_STAMPS_LIB", "1")
+stamps_lib = os.path.join(os.path.dirname(N.LIB_PATH), "libddrl_hip_stamps.so" if _sl in ("", "1") else _sl)
 if "--build" in sys.argv or not os.environ.get("DDRL_STAMPS_LIB"):
     lib = build.build(extra_flags=["-DDDRL_STAMPS"] + extra,
                       lib=stamps_lib if "--build" in sys.argv else

@@ -1,5 +1,5 @@
 """HBM traffic per minibatch step of the update kernels from the rocprofv3 PMC passes of
-tools/profile_r02.sh (FETCH_SIZE and WRITE_SIZE in separate runs, kB per dispatch).
+tools/profile_r02.sh / profile_r03.sh (FETCH_SIZE and WRITE_SIZE in separate runs, kB per dispatch).
 
     python tools/pmc_summary.py gpurun_out/prof > profiles/r02/pmc_summary.json
 
@@ -19,7 +19,7 @@ WORKLOADS = {
               "workload": "QuantrupedMultiEnv_Local, 4096 envs, T=200 (one fused launch: 10 x 6400 steps x 4 policies)"},
     "c4": {"kernels": ["void k_update_ffn<2, 5"], "steps": 10 * 25600,
            "workload": "QuantrupedMultiEnv_SharedDecentral, 4096 envs, T=200 (one fused launch: 10 x 25600 steps)"},
-    "c5": {"kernels": ["void k_gnn<2, 2>", "k_gnn_reduce", "k_gnn_adam", "k_gnn_gather"], "steps": 10 * 800,
+    "c5": {"kernels": ["void k_gnn<2, 2", "k_gnn_reduce", "k_gnn_adam", "k_gnn_gather"], "steps": 10 * 800,
            "workload": "QuantrupedMultiEnv_DecentralShared_Graph, 128 envs, T=200 (10 x 800 steps, 3 launches "
                        "each, plus one record gather per 1024 steps)"},
 }
@@ -36,7 +36,7 @@ def counter(path, name, prefix):
 
 
 def main(d):
-    out = {"command": "tools/profile_r02.sh: rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE (separate passes) -- "
+    out = {"command": "tools/profile_r0N.sh: rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE (separate passes) -- "
                       "python3 bench.py --steps 1 --warmup 0 ...",
            "gfx950_fetch_correction": GFX950_FETCH_CORRECTION, "workloads": {}}
     for name, w in WORKLOADS.items():
