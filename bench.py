@@ -38,14 +38,14 @@ def metric_name(envs):
     return f"env-steps/sec at {envs} envs × 4 leg agents; PPO update ms/minibatch"
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense FP32 (MFMA f32 = vector rate), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03", "pmc_summary.json")
 PMC_WORKLOAD = {"QuantrupedMultiEnv_Local": "local", "QuantrupedMultiEnv_SharedDecentral": "c4",
                 "QuantrupedMultiEnv_DecentralShared_Graph": "c5"}
 
 
 def pmc_traffic(env, policy_steps):
     """HBM bytes of the update (all its launches) from the committed rocprofv3 PMC passes
-    (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE; tools/profile_r02.sh): the
+    (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE; tools/profile_r03.sh): the
     workload's bytes per (policy, minibatch) step times this update's steps -- the kernels'
     traffic is per step.  The counters cannot be read live from inside the timed run; None
     for a workload without a committed pass."""
@@ -538,7 +538,7 @@ def main():
             "bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved_tf / PEAK_FP32_TFLOPS,
             "traffic": None if ddp else pmc_traffic(args.env, steps_per_policy * P),
-            "traffic_source": None if ddp else "profiles/r02/pmc_summary.json (bytes per step x steps of this update)",
+            "traffic_source": None if ddp else "profiles/r03/pmc_summary.json (bytes per step x steps of this update)",
             "algorithmic_flops_per_launch": flops_launch,
             "algorithmic_bytes_per_launch": rec_bytes_launch,
             "active_cus": active_cus,

@@ -29,7 +29,8 @@ def counter(path, name, prefix):
     tot, n = 0.0, 0
     with open(path) as f:
         for r in csv.DictReader(f):
-            if r["Counter_Name"] == name and r["Kernel_Name"].startswith(prefix):
+            kn = r["Kernel_Name"].replace("(anonymous namespace)::", "")   # r03: kernels in an unnamed namespace
+            if r["Counter_Name"] == name and kn.startswith(prefix):
                 tot += float(r["Counter_Value"])
                 n += 1
     return tot, n
