@@ -1,23 +1,25 @@
 // a13-a17: fused PPO minibatch SGD for the fcnet policy/value model (persistent kernel).
 //
-// Two workgroups per policy, on two CUs of one XCD: blockIdx = p + 8 branch, branch 0 = policy branch
-// (fc_1, fc_2, fc_out), branch 1 = value branch (fc_value_1, fc_value_2, value_out).  The
-// branches share no parameters, so each workgroup computes its own gradients and runs Adam
-// on its own parameters; the only coupling is tf.clip_by_global_norm, which needs the
-// squared norm over ALL variables: every step the two workgroups swap their partial
-// squared norms through one tagged 8-byte granule each (plain store / sc1 poll, slots double
-// buffered by step parity, zeroed by a memset before every launch, spins bounded).
-//
+// One launch runs the whole 10-epoch schedule of up to 4 policies.  Per policy the policy
+// branch (fc_1, fc_2, fc_out) and the value branch (fc_value_1, fc_value_2, value_out) each run
+// on KSP = 2 workgroups (the row split: 64 rows of the 128-row minibatch each, one 16-row MFMA
+// tile per wave, one wave per SIMD); blocks p, p + 8, p + 16, p + 24 (the dispatcher's
+// round robin puts them on one XCD, checked after every launch through HW_REG_XCC_ID).
+//   * the row halves swap their partial gradients every step through tagged 16-byte
+//     granules in the XCD's L2 (plain stores, sc1 polls; ppo_ffn_atomic.hip builds the same
+//     source with relaxed agent-scope atomics, valid for any placement);
+//   * the branches share only tf.clip_by_global_norm: one tagged 8-byte norm^2 granule
+//     each way per step.  Tags carry a 12-bit launch epoch, so no memset per launch.
 // Per minibatch step (RLlib TrainTFMultiGPU: row = shuffle[perm[e][b] * 128 + i]):
-//   rows of step s+1 are prefetched into registers while step s computes;
-//   forward of the branch for 32 rows per wave, one wave per SIMD (MFMA 16x16x4 f32,
-//   activations in registers, every weight operand read from LDS feeds two MFMAs);
-//   PPOLoss per row (RLlib 1.0 ppo_tf_policy.PPOLoss) and analytic dL/d(outputs);
-//   head / bias gradients and loss statistics by DPP row reductions (no LDS round trip);
-//   layer-2 backward from registers; H1/dZ2 then X/dZ1 through LDS for the two weight-
-//   gradient GEMMs (16x16 tiles, K = 128 rows); per-wave tile ownership;
-//   global-norm clip; tf1 Adam (ApplyAdam) with m / v held in registers by the owning
-//   lane and the weights updated in place in the LDS image.
+//   the step's records were gathered into LDS by LDS-DMA during the previous step;
+//   forward (MFMA 16x16x4 f32, activations in registers, weights in a swizzled LDS image);
+//   PPOLoss per row (RLlib 1.0) and dL/d(outputs); the policy head's dWo = H2^T dout as one
+//   more 16x16 tile of the dW2 MFMA stream and dH2 = Wo dout^T on MFMA, the value head's by
+//   DPP transpose-reductions; layer-2 backward from registers; H1/dZ2 then X/dZ1 through
+//   feature-major LDS images for the weight-gradient tiles (K = 64 rows), owned per wave;
+//   partner exchange; global-norm clip; tf1 Adam (m / v in the owning lanes' registers, two
+//   elements per packed instruction, weights updated in place in LDS).
+// ppo_ffn_impl.h holds the device code; DESIGN.md section 3 the measurements behind it.
 #include "ppo_ffn_impl.h"
 
 
