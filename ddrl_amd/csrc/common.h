@@ -144,10 +144,33 @@ __device__ __forceinline__ float row16_transpose_sum(float v[16]) {
   return keep + dpp_mov<0xB1>(send);     // quad_perm [1,0,3,2]
 }
 
+// Full wave64 sum of a double, in registers: the DPP row sum (xor 1, xor 2, half-mirror,
+// mirror) on both 32-bit halves, then the row pairs with the permlane swaps (xor 16, xor 32);
+// every lane gets the same bits (no ds_bpermute round trips as __shfl_xor of a double takes).
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov_d(double v) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)b, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(b >> 32), CTRL, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double xor_rows_sum_d(double v, bool x32) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
+  const auto rl = x32 ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                      : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto rh = x32 ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                      : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const double a = __builtin_bit_cast(double, ((unsigned long long)rh[0] << 32) | rl[0]);
+  const double c = __builtin_bit_cast(double, ((unsigned long long)rh[1] << 32) | rl[1]);
+  return a + c;
+}
 __device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_mov_d<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov_d<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov_d<0x141>(v);  // row_half_mirror
+  v += dpp_mov_d<0x140>(v);  // row_mirror
+  return xor_rows_sum_d(xor_rows_sum_d(v, false), true);
 }
 
 // ------------------------------------------------------------------------------------

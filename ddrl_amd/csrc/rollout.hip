@@ -26,9 +26,24 @@ __global__ void __launch_bounds__(256) k_filter_push(const float* __restrict__ o
   __shared__ double sh_mean;
   const int tid = threadIdx.x, w = tid >> 6;
   double mean_b = 0.0, s_b = 0.0;
+  // up to 256 * FMAXV rows: this thread's column values stay in registers between the two
+  // passes (all loads issued at once, no second pass over memory); larger batches reload
+  constexpr int FMAXV = 32;
+  float xv[FMAXV];
+  const bool cached = N <= 256 * FMAXV;
   if (enabled && update) {
     double acc = 0.0;
-    for (int e = tid; e < N; e += 256) acc += (double)obs[(size_t)e * D + j];
+    if (cached) {
+#pragma unroll
+      for (int i = 0; i < FMAXV; ++i) {
+        const int e = tid + 256 * i;
+        xv[i] = e < N ? obs[(size_t)e * D + j] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < FMAXV; ++i) acc += (double)xv[i];   // + 0.0 past N: the same sum
+    } else {
+      for (int e = tid; e < N; e += 256) acc += (double)obs[(size_t)e * D + j];
+    }
     acc = wave_sum_d(acc);
     if ((tid & 63) == 0) red[w] = acc;
     __syncthreads();
@@ -36,9 +51,18 @@ __global__ void __launch_bounds__(256) k_filter_push(const float* __restrict__ o
     __syncthreads();
     mean_b = sh_mean;
     double acc2 = 0.0;
-    for (int e = tid; e < N; e += 256) {
-      double dlt = (double)obs[(size_t)e * D + j] - mean_b;
-      acc2 += dlt * dlt;
+    if (cached) {
+#pragma unroll
+      for (int i = 0; i < FMAXV; ++i) {
+        if (tid + 256 * i >= N) break;
+        const double dlt = (double)xv[i] - mean_b;
+        acc2 += dlt * dlt;
+      }
+    } else {
+      for (int e = tid; e < N; e += 256) {
+        double dlt = (double)obs[(size_t)e * D + j] - mean_b;
+        acc2 += dlt * dlt;
+      }
     }
     acc2 = wave_sum_d(acc2);
     __syncthreads();
