@@ -404,8 +404,8 @@ def main():
                 ctx.params_set(p, uctx.params_get(p))
         # RLlib: update_kl with the last epoch's mean KL of every policy
         for p in range(P):
-            st = lctx.ppo_stats(p, E * nb[p])
-            mkl = float(np.mean(st[-nb[p]:, 3]))
+            st = lctx.ppo_stats(p, nb[p], first=(E - 1) * nb[p])   # the last epoch's rows
+            mkl = float(np.mean(st[:, 3]))
             kl[p] = kl[p] * 1.5 if mkl > 2 * 0.01 else (kl[p] * 0.5 if mkl < 0.5 * 0.01 else kl[p])
         if record:
             upd_ms.append(ev_upd[0].elapsed_time(ev_upd[1]))

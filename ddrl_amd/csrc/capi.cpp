@@ -843,11 +843,16 @@ int ddrl_ppo_update(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const 
 }
 
 int ddrl_ppo_stats(ddrl_ctx* c, int pid, float* host, size_t n_steps) {
+  return ddrl_ppo_stats_range(c, pid, 0, n_steps, host);
+}
+
+int ddrl_ppo_stats_range(ddrl_ctx* c, int pid, size_t first, size_t n_steps, float* host) {
   CHK_CTX(c);
   if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
+  if (!host && n_steps) return fail("null stats buffer");
   const size_t cap = (size_t)c->cfg.num_sgd_iter * c->pol[pid].nb;
-  if (n_steps > cap) return fail("more stats requested than the schedule holds");
-  HIPCHK(hipMemcpyAsync(host, c->pol[pid].stats, n_steps * 8 * 4, hipMemcpyDeviceToHost, c->stream));
+  if (first > cap || n_steps > cap - first) return fail("more stats requested than the schedule holds");
+  HIPCHK(hipMemcpyAsync(host, c->pol[pid].stats + first * 8, n_steps * 8 * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   if (check_err(c)) return -1;
   // the policy / value workgroups each write their own columns; total_loss is their

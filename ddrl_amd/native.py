@@ -79,6 +79,7 @@ _SIGS = {
     "ddrl_gae": ([VP], C.c_int),
     "ddrl_ppo_update": ([VP, C.c_int, C.POINTER(VP), C.POINTER(VP), C.POINTER(f32), C.c_int], C.c_int),
     "ddrl_ppo_stats": ([VP, C.c_int, VP, C.c_size_t], C.c_int),
+    "ddrl_ppo_stats_range": ([VP, C.c_int, C.c_size_t, C.c_size_t, VP], C.c_int),
     "ddrl_ppo_grad": ([VP, C.c_int, VP, C.c_int, f32, VP, C.c_int], C.c_int),
     "ddrl_ppo_apply": ([VP, C.c_int, VP], C.c_int),
     "ddrl_comm_unique_id": ([VP, C.c_size_t], C.c_int),
@@ -368,9 +369,10 @@ class Context:
         kl = (f32 * MAX_P)(*[float(k) for k in kl_coeffs])
         _ck(self.lib.ddrl_ppo_update(self.h, mask, sh, pe, kl, max_steps))
 
-    def ppo_stats(self, pid, n_steps):
+    def ppo_stats(self, pid, n_steps, first=0):
+        """Learner statistics rows [first, first + n_steps) of the last update (8 floats each)."""
         a = np.empty((n_steps, 8), np.float32)
-        _ck(self.lib.ddrl_ppo_stats(self.h, pid, a.ctypes.data, n_steps))
+        _ck(self.lib.ddrl_ppo_stats_range(self.h, pid, first, n_steps, a.ctypes.data))
         return a
 
     def ppo_grad(self, pid, rows_dev, n_rows, kl_coeff, grad_dev, stats_step=-1):

@@ -245,8 +245,8 @@ class PPOTrainer:
         self.ctx.ppo_update((1 << P) - 1, sh, pe, self.kl_coeff)
         learner = {}
         for p, pid in enumerate(self.policy_ids):
-            st = self.ctx.ppo_stats(p, self.cfg.num_sgd_iter * nbs[p])
-            last = st[-nbs[p]:].astype(np.float64).mean(0)   # TrainTFMultiGPU: last epoch's mean
+            st = self.ctx.ppo_stats(p, nbs[p], first=(self.cfg.num_sgd_iter - 1) * nbs[p])
+            last = st.astype(np.float64).mean(0)   # TrainTFMultiGPU: last epoch's mean
             learner[pid] = {"cur_kl_coeff": float(np.float32(self.kl_coeff[p])),
                             "cur_lr": float(np.float32(self.cfg.lr)),
                             "total_loss": last[0], "policy_loss": last[1], "vf_loss": last[2],

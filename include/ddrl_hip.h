@@ -212,6 +212,9 @@ int ddrl_ppo_update(ddrl_ctx* ctx, int pid_mask, const int32_t* const* shuffle_d
 /* Per-minibatch learner stats of the last update: n_steps x 8 floats
  * {total_loss, policy_loss, vf_loss, kl, entropy, vf_explained_var, grad_gnorm, clip_scale}. */
 int ddrl_ppo_stats(ddrl_ctx* ctx, int pid, float* host, size_t n_steps);
+/* Rows [first, first + n_steps) of the same statistics: RLlib's learner stats and update_kl
+ * (3p ppo.py update_kl, on the last epoch's mean KL) need only the last epoch's nb rows. */
+int ddrl_ppo_stats_range(ddrl_ctx* ctx, int pid, size_t first, size_t n_steps, float* host);
 
 /* Data-parallel (shared policy) primitives: gradient of (1/minibatch) * sum over the
  * given rows -> grad_dev[n_params]; after the caller's all-reduce (RCCL), apply clip +

@@ -243,6 +243,10 @@ def test_full_schedule_runs_and_stays_close():
     strict_params_check(got, "ffn", params[p], shapes, batch, sh, pe, 0.2, 20, msg="full schedule")
     st = ctx.ppo_stats(p, 20)
     _close(st[-1, 0], stats[-1]["total_loss"], rtol=1e-3, atol=1e-4)
+    # the last epoch's rows alone (what update_kl reads) are the same rows of the full read
+    np.testing.assert_array_equal(ctx.ppo_stats(p, 2, first=18), st[18:])
+    with pytest.raises(N.DdrlError):
+        ctx.ppo_stats(p, 3, first=18)              # past the 10 x 2 schedule
     ctx.close()
 
 
