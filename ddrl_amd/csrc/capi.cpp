@@ -217,7 +217,7 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
          dalloc(c, &P.v, P.n_params) || dalloc(c, &P.beta_pow, 4) || dalloc(c, &P.grad, P.n_params) ||
          dalloc(c, &P.rec, (size_t)P.R * P.lay.stride) || dalloc(c, &P.stage, stage_n) ||
          dalloc(c, &P.last_v, P.C) || dalloc(c, &P.adv_norm, 2) ||
-         dalloc(c, &P.partials, 2 * (size_t)((P.C + 255) / 256) + 4) ||
+         dalloc(c, &P.partials, (size_t)gae_partials_len(P.C)) ||
          dalloc(c, &P.stats, (size_t)g.num_sgd_iter * P.nb * 8);
     if (!rc) {
       // beta1^t, beta2^t, then the arrival counter of the multi-workgroup apply kernel (0)
@@ -238,7 +238,7 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
        dalloc(c, &c->h_obs, (size_t)N * g.obs_full_dim) ||
        dalloc(c, &c->h_eps, (size_t)N * g.n_agents * g.act_dim) || dalloc(c, &c->h_act, (size_t)N * 8) ||
        dalloc(c, &c->h_fw, N) || dalloc(c, &c->h_cfrc, (size_t)N * 14 * 6) || dalloc(c, &c->h_done, N);
-  for (int p = 0; p < g.n_policies && !rc && g.model_kind == DDRL_MODEL_FFN; ++p)
+  for (int p = 0; p < g.n_policies && !rc; ++p)
     rc = dalloc(c, &c->snap[p], 3 * (size_t)c->pol[p].n_params + 4);
   if (const char* e = std::getenv("DDRL_XCHG")) c->xchg_atomic = std::string(e) == "atomic" ? 1 : 0;
   if (const char* e = std::getenv("DDRL_TEST_FAIL_STEP")) c->fail_step = std::atoi(e);
@@ -758,14 +758,16 @@ int ddrl_rollout_hostenv(ddrl_ctx* c, ddrl_hostenv* env, int groups, const float
 int ddrl_gae(ddrl_ctx* c) {
   CHK_CTX(c);
   const ddrl_cfg& g = c->cfg;
+  GaeBatch gb{};
+  gb.P = g.n_policies;
   for (int p = 0; p < g.n_policies; ++p) {
     Policy& P = c->pol[p];
-    GaeArgs ga{};
+    GaeArgs& ga = gb.g[p];
     ga.rec = P.rec; ga.lay = P.lay; ga.C = P.C; ga.T = g.frag_len; ga.N = g.n_envs; ga.k = P.k;
     ga.last_v = P.last_v; ga.done_tn = c->done_tn; ga.gamma = g.gamma; ga.lambda_ = g.lambda_;
     ga.partials = P.partials; ga.adv_norm = P.adv_norm;
-    launch_gae(c->stream, ga);
   }
+  launch_gae(c->stream, gb);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -826,6 +828,10 @@ int ddrl_ppo_update(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const 
     const int last = c->pol[0].last_steps;
     if (!c->gnn.chunk && dalloc(c, &c->gnn.chunk, (size_t)c->gnn.chunk_steps * DDRL_MB * c->pol[0].lay.stride))
       return -1;
+    if (snapshot(c, 1)) return -1;
+    // test hook (DDRL_TEST_FAIL_STEP): the update starts with the error word set, as a failed
+    // launch would leave it; the steps run, check_err restores the snapshot
+    if (c->fail_step >= 0) (void)hipMemsetD32Async((hipDeviceptr_t)c->err, 1, 1, c->stream);
     const int CH = c->gnn.chunk_steps;
     // the records of each run of GNN_CHUNK_STEPS steps are gathered into one contiguous
     // chunk first (stream order: after the previous run's last step), so every gradient

@@ -9,7 +9,7 @@
 // recursion y_t = delta_t + gamma*lambda*y_{t+1} (reset after a done) is exactly lfilter's.
 // One thread per chain; the loads over t are coalesced across chains (time-major rows).
 // StandardizeFields: (adv - mean) / max(1e-4, std) over the policy's whole batch; the sums
-// are fp64 and reduced in a fixed order (per-block partials + one finalize block).
+// are fp64 and reduced in a fixed order (per-wave partials + one finalize block per policy).
 #include "common.h"
 #include "kernels.h"
 
@@ -58,8 +58,16 @@ __device__ __forceinline__ void gae_run(const GaeArgs& g, int c, int t0, const G
   }
 }
 
-__global__ void __launch_bounds__(256) k_gae(GaeArgs g) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+// One launch for all policies (blockIdx.y), one wave per block: a policy's C chains spread
+// over C / 64 workgroups (Local at 4096 envs: 256 CUs busy instead of 16, whose texture units
+// serialized the strided record loads; 4 x 255 -> one ~60 us launch).  Each block writes its
+// wave's (sum adv, sum adv^2); the finalize sums them four at a time as ((w0 + w1) + (w2 + w3))
+// and then over the groups in order -- the 256-thread reduction's order, so adv_norm and the
+// totals are bit-identical to it.
+__global__ void __launch_bounds__(64) k_gae(GaeBatch gb) {
+  const GaeArgs& g = gb.g[blockIdx.y];
+  if ((int)blockIdx.x * 64 >= g.C) return;
+  const int c = blockIdx.x * 64 + threadIdx.x;
   double s1 = 0.0, s2 = 0.0;
   if (c < g.C) {
     const int e = c / g.k;
@@ -77,32 +85,37 @@ __global__ void __launch_bounds__(256) k_gae(GaeArgs g) {
       gae_run(g, c, tb, b, acc, nextv, s1, s2);
     }
   }
-  __shared__ double red[2][4];
   s1 = wave_sum_d(s1);
   s2 = wave_sum_d(s2);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) {
-    red[0][w] = s1;
-    red[1][w] = s2;
-  }
-  __syncthreads();
   if (threadIdx.x == 0) {
-    g.partials[2 * blockIdx.x] = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-    g.partials[2 * blockIdx.x + 1] = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    double* wp = g.partials + gae_wave_base(g.C) + 2 * blockIdx.x;
+    wp[0] = s1;
+    wp[1] = s2;
   }
 }
 
-__global__ void k_gae_finalize(GaeArgs g, int nblocks) {
+__global__ void k_gae_finalize(GaeBatch gb) {
   if (threadIdx.x != 0) return;
+  const GaeArgs& g = gb.g[blockIdx.x];
+  const int nw = (g.C + 63) / 64, ngroups = (g.C + 255) / 256;
+  const double* wp = g.partials + gae_wave_base(g.C);
   double s1 = 0.0, s2 = 0.0;
-  for (int b = 0; b < nblocks; ++b) {
-    s1 += g.partials[2 * b];
-    s2 += g.partials[2 * b + 1];
+  for (int b = 0; b < ngroups; ++b) {
+    double x[2][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int w = 4 * b + i;
+      x[0][i] = w < nw ? wp[2 * w] : 0.0;
+      x[1][i] = w < nw ? wp[2 * w + 1] : 0.0;
+    }
+    s1 += (x[0][0] + x[0][1]) + (x[0][2] + x[0][3]);
+    s2 += (x[1][0] + x[1][1]) + (x[1][2] + x[1][3]);
   }
   const double n = (double)g.C * (double)g.T;
-  g.partials[2 * nblocks] = s1;        // for a cross-rank StandardizeFields
-  g.partials[2 * nblocks + 1] = s2;
-  g.partials[2 * nblocks + 2] = n;
+  double* tot = g.partials + 2 * ngroups;   // for a cross-rank StandardizeFields
+  tot[0] = s1;
+  tot[1] = s2;
+  tot[2] = n;
   const double mean = s1 / n;
   double var = s2 / n - mean * mean;
   if (var < 0.0) var = 0.0;
@@ -111,8 +124,9 @@ __global__ void k_gae_finalize(GaeArgs g, int nblocks) {
   g.adv_norm[1] = fmaxf(1e-4f, std32);
 }
 
-void launch_gae(hipStream_t s, const GaeArgs& g) {
-  const int nblocks = (g.C + 255) / 256;
-  hipLaunchKernelGGL(k_gae, dim3(nblocks), dim3(256), 0, s, g);
-  hipLaunchKernelGGL(k_gae_finalize, dim3(1), dim3(64), 0, s, g, nblocks);
+void launch_gae(hipStream_t s, const GaeBatch& gb) {
+  int maxw = 1;
+  for (int p = 0; p < gb.P; ++p) maxw = maxw > (gb.g[p].C + 63) / 64 ? maxw : (gb.g[p].C + 63) / 64;
+  hipLaunchKernelGGL(k_gae, dim3(maxw, gb.P), dim3(64), 0, s, gb);
+  hipLaunchKernelGGL(k_gae_finalize, dim3(gb.P), dim3(64), 0, s, gb);
 }

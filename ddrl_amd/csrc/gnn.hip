@@ -38,6 +38,7 @@
 // Training steps are three launches: per-tile partial gradients (k_gnn<MODE_GRAD>), a
 // fixed-order reduction over tiles + squared norm partials (k_gnn_reduce), and
 // clip_by_global_norm + tf1 Adam (k_gnn_adam).  A DDP step stops after the reduction.
+// (Reduction and Adam fused into one launch behind a grid barrier measured slower: DESIGN §3.)
 #include "common.h"
 #include "kernels.h"
 #include "ppo_loss.h"

@@ -104,10 +104,15 @@ struct GaeArgs {
   float* rec; RecLayout lay; int C, T, N, k;
   const float* last_v; const uint8_t* done_tn;
   double gamma, lambda_;
-  double* partials;   // [nblocks][2] + totals {sum adv, sum adv^2, count} after the blocks
+  // totals {sum adv, sum adv^2, count} at [2 * ceil(C / 256)], per-wave partial sums
+  // [ceil(C / 64)][2] from gae_wave_base(C); gae_partials_len(C) doubles in all
+  double* partials;
   float* adv_norm;    // [2]: mean, max(1e-4, std)
 };
-void launch_gae(hipStream_t s, const GaeArgs& g);
+__host__ __device__ inline int gae_wave_base(int C) { return 2 * ((C + 255) / 256) + 4; }
+__host__ __device__ inline int gae_partials_len(int C) { return gae_wave_base(C) + 2 * ((C + 63) / 64); }
+struct GaeBatch { GaeArgs g[DDRL_MAXP]; int P; };
+void launch_gae(hipStream_t s, const GaeBatch& gb);   // every policy of the context, one launch
 
 // ---- PPO update (fused persistent minibatch loop) ----
 struct UpdateArgs {
