@@ -62,6 +62,7 @@ struct ddrl_ctx {
   RouteArgs route{};
   double *f_n = nullptr, *f_M = nullptr, *f_S = nullptr, *f_normc = nullptr;
   double *f_dn = nullptr, *f_dM = nullptr, *f_dS = nullptr;   // pushes since the last sync
+  double* f_part = nullptr;                                     // filter push chunk scratch
   double* pf = nullptr;   // per-policy RLlib MeanStdFilter state [P][PF_STRIDE]
   double* zs = nullptr;   // fp64 column sums of the env-normalized observation [2][D]
   uint8_t* done_tn = nullptr;
@@ -230,6 +231,7 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
   rc = rc || dalloc(c, &c->f_n, 1) || dalloc(c, &c->f_M, DDRL_MAXFULL) || dalloc(c, &c->f_S, DDRL_MAXFULL) ||
        dalloc(c, &c->f_normc, 2 * DDRL_MAXFULL) || dalloc(c, &c->f_dn, 1) ||
        dalloc(c, &c->f_dM, DDRL_MAXFULL) || dalloc(c, &c->f_dS, DDRL_MAXFULL) ||
+       dalloc(c, &c->f_part, filter_part_doubles(N, DDRL_MAXFULL)) ||
        dalloc(c, &c->pf, (size_t)DDRL_MAXP * PF_STRIDE) || dalloc(c, &c->zs, 2 * DDRL_MAXFULL) || dalloc(c, &c->done_tn, (size_t)T * N) ||
        dalloc(c, &c->stage_tab, DDRL_MAXP) || dalloc(c, &c->zero_perm, 4) ||
        dalloc(c, &c->xchg, 8 * DDRL_MAXP) ||
@@ -541,7 +543,7 @@ int ddrl_observe_range(ddrl_ctx* c, const float* obs, int e0, int e1) {
   ra.N = n;
   ra.e0 = e0;
   launch_filter_push(c->stream, obs_r, n, g.obs_full_dim, c->f_n, c->f_M, c->f_S, c->f_normc,
-                     g.filter_update, g.filter_enabled, c->f_dn, c->f_dM, c->f_dS);
+                     g.filter_update, g.filter_enabled, c->f_dn, c->f_dM, c->f_dS, c->f_part);
   const float clip = g.filter_enabled ? g.filter_clip : 0.f;
   if (g.policy_filter) launch_policy_filter(c->stream, ra, obs_r, c->f_normc, clip, c->zs, c->pf, 1);
   const FilterCount fc{c->f_n, c->f_dn, g.filter_enabled && g.filter_update ? n : 0};

@@ -18,7 +18,7 @@
 // The record loads of a chunk of GAE_U time steps are issued one chunk ahead of the
 // recursion (the stores of adv / vt may alias them as far as the compiler knows, so it would
 // otherwise wait for every load in turn: one memory round trip per time step).
-#define GAE_U 8
+#define GAE_U 16
 struct GaeChunk { float v[GAE_U], r[GAE_U]; bool d[GAE_U]; };
 
 __device__ __forceinline__ void gae_load(const GaeArgs& g, int c, int e, int t0, GaeChunk& ch) {

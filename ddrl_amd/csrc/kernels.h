@@ -38,9 +38,11 @@ struct RouteArgs {
 
 // ---- filter / observe (rollout.hip) ----
 // dn / dM / dS: a second running stat of the pushes since the last cross-rank filter sync
+// part: filter_part_doubles(N, D) doubles of per-chunk (mean, M2) scratch
 void launch_filter_push(hipStream_t s, const float* obs, int N, int D, double* n_run, double* M,
                         double* S, double* normc, int update, int enabled, double* dn, double* dM,
-                        double* dS);
+                        double* dS, double* part);
+size_t filter_part_doubles(int N, int D);
 // the batch count of the env-side filter push, added by the observe kernel
 struct FilterCount { double* n_run; double* dn; int count; };
 // pf: per-policy RLlib MeanStdFilter state (PF_* layout, nullptr when disabled)
