@@ -92,6 +92,13 @@ struct ddrl_ctx {
   ncclComm_t comm = nullptr;           // data-parallel learner (ddrl_comm_init)
   float *h_fw = nullptr, *h_cfrc = nullptr;
   uint8_t* h_done = nullptr;
+  // ddrl_rollout_fragment as one HIP graph (T x (act, reward, filter push, observe) +
+  // bootstrap), captured on first use and re-used while the call's buffers are the same
+  // (every other kernel argument is fixed at context creation); DDRL_ROLLOUT_GRAPH=0: launches
+  int rollout_graph = 1;
+  hipGraphExec_t rg_exec = nullptr;
+  hipStream_t cap_stream = nullptr;    // capture only (the caller's stream may be the null stream)
+  const void* rg_key[6] = {nullptr};
   std::vector<void*> allocs;
 };
 
@@ -244,6 +251,7 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
     rc = dalloc(c, &c->snap[p], 3 * (size_t)c->pol[p].n_params + 4);
   if (const char* e = std::getenv("DDRL_XCHG")) c->xchg_atomic = std::string(e) == "atomic" ? 1 : 0;
   if (const char* e = std::getenv("DDRL_TEST_FAIL_STEP")) c->fail_step = std::atoi(e);
+  if (const char* e = std::getenv("DDRL_ROLLOUT_GRAPH")) c->rollout_graph = std::atoi(e) != 0;
   if (!rc && g.model_kind == DDRL_MODEL_GNN) {
     const int np = c->pol[0].n_params;
     c->gnn.part_stride = (np + 3) & ~3;   // 16-byte aligned tile rows (float4 partial stores)
@@ -274,6 +282,8 @@ int ddrl_ctx_destroy(ddrl_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
   if (c->comm) (void)ncclCommDestroy(c->comm);
+  if (c->rg_exec) (void)hipGraphExecDestroy(c->rg_exec);
+  if (c->cap_stream) (void)hipStreamDestroy(c->cap_stream);
   for (void* p : c->allocs) (void)hipFree(p);
   delete c;
   return 0;
@@ -641,10 +651,8 @@ int ddrl_reward_range(ddrl_ctx* c, int t, int e0, int e1, const float* fw, const
   return 0;
 }
 
-int ddrl_rollout_fragment(ddrl_ctx* c, const float* obs, const float* eps, const float* fw, const float* cfrc,
-                          const uint8_t* done, float* actions) {
-  CHK_CTX(c);
-  if (!obs || !eps || !fw || !cfrc || !actions) return fail("null rollout buffer");
+static int rollout_launches(ddrl_ctx* c, const float* obs, const float* eps, const float* fw, const float* cfrc,
+                            const uint8_t* done, float* actions) {
   const ddrl_cfg& g = c->cfg;
   const size_t N = g.n_envs;
   for (int t = 0; t < g.frag_len; ++t) {
@@ -654,6 +662,47 @@ int ddrl_rollout_fragment(ddrl_ctx* c, const float* obs, const float* eps, const
     if (ddrl_observe(c, obs + (size_t)(t + 1) * N * g.obs_full_dim)) return -1;
   }
   return ddrl_bootstrap(c);
+}
+
+int ddrl_rollout_fragment(ddrl_ctx* c, const float* obs, const float* eps, const float* fw, const float* cfrc,
+                          const uint8_t* done, float* actions) {
+  CHK_CTX(c);
+  if (!obs || !eps || !fw || !cfrc || !actions) return fail("null rollout buffer");
+  if (!c->rollout_graph) return rollout_launches(c, obs, eps, fw, cfrc, done, actions);
+  const void* key[6] = {obs, eps, fw, cfrc, done, actions};
+  if (!c->rg_exec || !std::equal(key, key + 6, c->rg_key)) {
+    if (c->rg_exec) {
+      HIPCHK(hipGraphExecDestroy(c->rg_exec));
+      c->rg_exec = nullptr;
+    }
+    // captured on a private stream (a capture records, it does not run), launched on the caller's
+    if (!c->cap_stream) HIPCHK(hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking));
+    const hipStream_t user = c->stream;
+    c->stream = c->cap_stream;
+    hipError_t e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal);
+    if (e != hipSuccess) {
+      c->stream = user;
+      return fail(std::string("rollout graph capture: ") + hipGetErrorString(e));
+    }
+    const int rc = rollout_launches(c, obs, eps, fw, cfrc, done, actions);
+    hipGraph_t graph = nullptr;
+    e = hipStreamEndCapture(c->stream, &graph);
+    c->stream = user;
+    if (rc) {
+      if (graph) (void)hipGraphDestroy(graph);
+      return -1;
+    }
+    if (e != hipSuccess) return fail(std::string("rollout graph capture: ") + hipGetErrorString(e));
+    const hipError_t ei = hipGraphInstantiate(&c->rg_exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (ei != hipSuccess) {
+      c->rg_exec = nullptr;
+      return fail(std::string("rollout graph instantiate: ") + hipGetErrorString(ei));
+    }
+    std::copy(key, key + 6, c->rg_key);
+  }
+  HIPCHK(hipGraphLaunch(c->rg_exec, c->stream));
+  return 0;
 }
 
 int ddrl_step_host(ddrl_ctx* c, int t, const float* obs_h, const float* eps_h, float* act_h) {

@@ -28,6 +28,8 @@ class SyntheticRollout:
 
     def dones_for_fragment(self):
         t = torch.arange(self.T, device=self.phase.device)[:, None] + self.t_global
-        self.done = (((t + self.phase[None, :]) % 1000) == 999).to(torch.uint8)
+        # in place: the buffer keeps its address, so the library's captured rollout graph
+        # (keyed by the buffers of the call) is re-used
+        self.done.copy_(((t + self.phase[None, :]) % 1000) == 999)
         self.t_global += self.T
         return self.done
