@@ -54,30 +54,15 @@ __global__ void k_filter_merge(int N, int D, const double* __restrict__ part, do
   double n1 = n_run[0];
   double Mj = M[j], Sj = S[j];
   if (push) {
-    // the batch's (mean, M2): the chunks merged in order (Chan et al.); the first FP_PRE
-    // chunks' partials are loaded up front (one L2 round trip, not one per chunk)
-    constexpr int FP_PRE = 16;
+    // the batch's (mean, M2): the chunks merged in order (Chan et al.)
     const int nchunks = (N + FP_ROWS - 1) / FP_ROWS;
-    double pm[FP_PRE], ps[FP_PRE];
-#pragma unroll
-    for (int c = 0; c < FP_PRE; ++c) {
-      const double* pc = part + ((size_t)c * D + j) * 2;
-      pm[c] = c < nchunks ? pc[0] : 0.0;
-      ps[c] = c < nchunks ? pc[1] : 0.0;
-    }
     double nb = 0.0, mean_b = 0.0, s_b = 0.0;
-    auto merge = [&](int c, double mc, double sq) {
-      const double nc = (double)min(FP_ROWS, N - c * FP_ROWS), nn = nb + nc, d = mc - mean_b;
-      mean_b = (nb * mean_b + nc * mc) / nn;
-      s_b = s_b + sq + d * d * nb * nc / nn;
-      nb = nn;
-    };
-#pragma unroll
-    for (int c = 0; c < FP_PRE; ++c)
-      if (c < nchunks) merge(c, pm[c], ps[c]);
-    for (int c = FP_PRE; c < nchunks; ++c) {
+    for (int c = 0; c < nchunks; ++c) {
       const double* pc = part + ((size_t)c * D + j) * 2;
-      merge(c, pc[0], pc[1]);
+      const double nc = (double)min(FP_ROWS, N - c * FP_ROWS), nn = nb + nc, d = pc[0] - mean_b;
+      mean_b = (nb * mean_b + nc * pc[0]) / nn;
+      s_b = s_b + pc[1] + d * d * nb * nc / nn;
+      nb = nn;
     }
     const double n2 = (double)N, n = n1 + n2;
     const double delta = Mj - mean_b;
