@@ -155,7 +155,9 @@ int ddrl_reward_range(ddrl_ctx* ctx, int t, int e0, int e1, const float* fw_dev,
  * bootstrap.  Expects observe(obs_dev[0]) to have been called.  Layouts: obs_dev[T+1][N][D],
  * eps_dev[T][N][n_agents][A], fw_dev[T][N], cfrc_dev[T][N][14][6], done_dev[T][N] (may be
  * NULL), actions_dev[N][8] (scratch: the env actions of the last step).  One call instead of
- * 3 T host calls: the per-step launches stay in C++. */
+ * 3 T host calls: the per-step launches stay in C++, captured once into a HIP graph that is
+ * re-launched while the six buffer pointers are unchanged (contents may change between calls;
+ * DDRL_ROLLOUT_GRAPH=0 at context creation issues the launches directly). */
 int ddrl_rollout_fragment(ddrl_ctx* ctx, const float* obs_dev, const float* eps_dev, const float* fw_dev,
                           const float* cfrc_dev, const uint8_t* done_dev, float* actions_dev);
 /* Host-buffer variants for a host-side env (MultiAgentEnv.step on host cores): pinned
