@@ -38,24 +38,48 @@ def metric_name(envs):
     return f"env-steps/sec at {envs} envs × 4 leg agents; PPO update ms/minibatch"
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense FP32 (MFMA f32 = vector rate), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03", "pmc_summary.json")
+PMC_SUMMARIES = [os.path.join(ROOT, "profiles", r, "pmc_summary.json") for r in ("r04", "r03")]
 PMC_WORKLOAD = {"QuantrupedMultiEnv_Local": "local", "QuantrupedMultiEnv_SharedDecentral": "c4",
                 "QuantrupedMultiEnv_DecentralShared_Graph": "c5"}
 
 
+def pmc_summary():
+    """The newest committed rocprofv3 PMC summary (tools/pmc_summary.py) and its path."""
+    for path in PMC_SUMMARIES:
+        try:
+            with open(path) as f:
+                return json.load(f), os.path.relpath(path, ROOT)
+        except OSError:
+            continue
+    return None, None
+
+
+def pmc_workload(env):
+    s, path = pmc_summary()
+    w = (s or {}).get("workloads", {}).get(PMC_WORKLOAD.get(env, ""))
+    return w, path
+
+
 def pmc_traffic(env, policy_steps):
     """HBM bytes of the update (all its launches) from the committed rocprofv3 PMC passes
-    (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE; tools/profile_r03.sh): the
+    (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE; tools/profile_r04.sh): the
     workload's bytes per (policy, minibatch) step times this update's steps -- the kernels'
     traffic is per step.  The counters cannot be read live from inside the timed run; None
     for a workload without a committed pass."""
-    try:
-        with open(PMC_SUMMARY) as f:
-            s = json.load(f)
-    except OSError:
-        return None
-    w = s.get("workloads", {}).get(PMC_WORKLOAD.get(env, ""))
+    w, _ = pmc_workload(env)
     return w["hbm_bytes_per_step"] * policy_steps if w else None
+
+
+def pmc_mfma(env):
+    """MFMA-busy and effective clock of the workload's dominant update kernel from the committed
+    counter pass (SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE with --kernel-trace; see
+    tools/pmc_summary.py for the arithmetic), or {} without one."""
+    w, path = pmc_workload(env)
+    m = (w or {}).get("mfma")
+    if not m:
+        return {}
+    return {"mfma_busy_frac": m.get("mfma_busy_frac_of_active_simds"), "clock_ghz": m.get("clock_ghz"),
+            "mfma_busy_frac_chip": m.get("mfma_busy_frac_chip"), "mfma_source": f"{path} ({m.get('kernel')})"}
 
 
 def ffn_flops_per_row(d, A, H=64):
@@ -439,15 +463,16 @@ def main():
 
     pcie = None
     if world == 1 and not args.no_pcie and not ddp:
-        # one more iteration with the envs on the host (not part of value): pipelined host env
+        # as many iterations again with the envs on the host (not part of value): pipelined host env
         # plane rollout + GAE + the same update
         torch.cuda.synchronize()
         rollout_host_env()            # warm-up: resets the envs, first pinned transfers
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        iteration(False, host_io=True)
+        for _ in range(args.steps):   # the same number of iterations as the timed region
+            iteration(False, host_io=True)
         torch.cuda.synchronize()
-        it_s = time.perf_counter() - t1
+        it_s = (time.perf_counter() - t1) / args.steps
         ro = {}
         for groups in (1, 2):
             torch.cuda.synchronize()
@@ -461,11 +486,12 @@ def main():
         step_s = (time.perf_counter() - t3) / 20
         per_step_bytes = 4 * n_local * (cfg.obs_full_dim + 8 + 1 + 14 * 6) + n_local
         pcie = {"value": T * n_local / it_s, "unit": "env-steps/s", "iteration_ms": it_s * 1e3,
+                "iterations": args.steps,
                 "rollout_ms": ro[2] * 1e3, "rollout_env_steps_per_s": T * n_local / ro[2],
                 "rollout_ms_unpipelined": ro[1] * 1e3, "host_env_step_ms": step_s * 1e3,
                 "host_threads": henv.threads, "env_groups": 2,
                 "pcie_bytes_per_vector_step": per_step_bytes,
-                "note": "one iteration with the envs stepped on the host: the C++ thread pool steps the "
+                "note": f"{args.steps} iterations (as many as value's) with the envs stepped on the host: the C++ thread pool steps the "
                         "clean-room QuAntruped stand-in (not MuJoCo) into pinned buffers, pipelined over 2 env "
                         "groups (ddrl_rollout_hostenv: one group's host step overlaps the other's device work "
                         "and PCIe transfers); rollout_ms_unpipelined = the same with one group; host_env_step_ms "
@@ -497,9 +523,15 @@ def main():
         active_cus = 2 * P * split
         model = f"{P} {'shared' if P == 1 else 'independent'} fcnet 2x64 polic{'y' if P == 1 else 'ies'} (d={d}, A={A})"
     # algorithmic HBM bytes: each minibatch row's record fields read once per branch
-    # (policy: obs, action, old logits, logp, adv; value: obs, vf, vt) + its shuffle index
+    # (policy: obs, action, old logits, logp, adv; value: obs, vf, vt) + its shuffle index.
+    # The fcnet launch keeps theta / Adam m, v on chip for the whole launch (LDS + registers),
+    # so its per-step bytes are the records; the GNN step is three launches, so every step also
+    # reads and writes theta, m, v (6 x 4 B per parameter) and writes + reads one gradient
+    # (2 x 4 B per parameter)
     obs_len = 93 if gnn else d
     rec_bytes_launch = 4 * (2 * obs_len + 3 * A + 4 + 2) * rows_per_step * steps_per_policy * P
+    if gnn:
+        rec_bytes_launch += (6 + 2) * 4 * ctx.n_params[0] * steps_per_policy * P
     ddp_how = ("RCCL all-reduce of the gradient every SGD step, loop in the library (ddrl_ppo_update_ddp)"
                if isinstance(learner, NativeDataParallelLearner) else
                f"{'RCCL' if backend == 'nccl' else backend} all-reduce of the gradient every SGD step, Python loop") \
@@ -538,11 +570,12 @@ def main():
             "bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved_tf / PEAK_FP32_TFLOPS,
             "traffic": None if ddp else pmc_traffic(args.env, steps_per_policy * P),
-            "traffic_source": None if ddp else "profiles/r03/pmc_summary.json (bytes per step x steps of this update)",
+            "traffic_source": None if ddp else f"{pmc_summary()[1]} (bytes per step x steps of this update)",
             "algorithmic_flops_per_launch": flops_launch,
             "algorithmic_bytes_per_launch": rec_bytes_launch,
             "active_cus": active_cus,
             "frac_of_active_cus": achieved_tf / (PEAK_FP32_TFLOPS * active_cus / 256),
+            **({} if ddp else pmc_mfma(args.env)),
         },
     }
     if pcie is not None:

@@ -104,13 +104,23 @@ constexpr int kTimeLimit = 1000;      // gym TimeLimit of the registered envs (s
 constexpr double kQ0[8] = {0.0, 1.0, 0.0, -1.0, 0.0, -1.0, 0.0, 1.0};   // rest pose (knees bent)
 constexpr double kGear = 30.0, kSpring = 8.0, kDamp = 1.5, kLimit = 1.4;
 constexpr double kShin = 0.7, kHipOff = 0.08, kGround = 400.0, kGroundDamp = 8.0;
+constexpr uint64_t kTvDraw = 1u << 20;   // counter index of the target-velocity draw (pose draws use 0..16)
 }  // namespace
 
-void ddrl_hostenv::reset_env(int e) {
+void ddrl_hostenv::reset_env(int e, bool draw_tv) {
   EnvState& s = st[e];
   const uint32_t ep = s.episode + 1;
+  const double tv = s.tv;
   std::memset(&s, 0, sizeof(s));
   s.episode = ep;
+  s.tv = tv;
+  if (draw_tv) {
+    // random.choice(target_velocity_list): every list position equally likely (a repeated value
+    // counts once per position); draw index kTvDraw of the episode's counter stream
+    const double u = 0.5 * (hostenv::hash_uniform(seed, e, ep, kTvDraw) + 1.0);   // [0, 1)
+    const size_t n = tv_list.size();
+    s.tv = tv_list[std::min(n - 1, (size_t)(u * (double)n))];
+  }
   int k = 0;
   s.z = 0.57 + 0.01 * hostenv::hash_uniform(seed, e, ep, k++);
   for (int j = 0; j < 8; ++j) {
@@ -134,7 +144,7 @@ void ddrl_hostenv::write_obs(int e, const double* ctrl) {
   for (double v : qvel) o[i++] = (float)v;
   for (int j = 0; j < 8; ++j) o[i++] = (float)s.qfrc[j];
   for (int j = 0; j < 8; ++j) o[i++] = (float)(ctrl ? ctrl[j] : 0.0);
-  if (D > 43) o[i++] = (float)target_velocity;
+  if (D > 43) o[i++] = (float)s.tv;
 }
 
 void ddrl_hostenv::step_env(int e, const float* a8) {
@@ -190,7 +200,7 @@ void ddrl_hostenv::step_env(int e, const float* a8) {
   // quantruped_v3.py:391-392)
   const double vx = (s.x - x0) / kDt;
   if (D > 43) {
-    const double tv = target_velocity;
+    const double tv = s.tv;
     fw[e] = (float)((1.0 + 1.0 / tv) * (1.0 / (std::fabs(vx - tv) + 1.0) - 1.0 / (tv + 1.0)));
   } else {
     fw[e] = (float)vx;
@@ -231,6 +241,12 @@ void ddrl_hostenv::reset_all() {
   });
 }
 
+void ddrl_hostenv::reset_state() {
+  pool->parallel_for(N, [this](int lo, int hi) {
+    for (int e = lo; e < hi; ++e) reset_env(e, false);   // steps = 0: the TimeLimit count restarts too
+  });
+}
+
 void ddrl_hostenv::step(int e0, int e1) {
   pool->parallel_for(e1 - e0, [this, e0](int lo, int hi) {
     for (int e = e0 + lo; e < e0 + hi; ++e) step_env(e, act + (size_t)e * 8);
@@ -254,7 +270,7 @@ extern "C" int ddrl_hostenv_create(int n_envs, int obs_dim, int n_threads, uint6
   h->N = n_envs;
   h->D = obs_dim;
   h->seed = seed;
-  h->target_velocity = target_velocity;
+  h->tv_list.assign(1, (double)target_velocity);
   h->st.assign(n_envs, EnvState{});
   const size_t N = n_envs;
   // pinned when a GPU is present (the DMA engines read / write them directly); without one
@@ -323,3 +339,37 @@ extern "C" int ddrl_hostenv_step(ddrl_hostenv* h, int e0, int e1) {
 }
 
 extern "C" int ddrl_hostenv_threads(ddrl_hostenv* h) { return h ? h->pool->size() : 0; }
+
+extern "C" int ddrl_hostenv_set_target_velocities(ddrl_hostenv* h, const float* list, int n) {
+  if (!h || !list || n < 1) {
+    g_henv_err = "ddrl_hostenv_set_target_velocities: a list of n >= 1 values";
+    return -1;
+  }
+  for (int i = 0; i < n; ++i) {
+    if (h->D > 43 && !(list[i] > 0.f)) {
+      g_henv_err = "ddrl_hostenv_set_target_velocities: obs_dim 44 needs target velocities > 0 "
+                   "(the TVel reward divides by it)";
+      return -1;
+    }
+  }
+  h->tv_list.assign(list, list + n);
+  return 0;
+}
+
+extern "C" int ddrl_hostenv_target_velocities(ddrl_hostenv* h, float* out, int n) {
+  if (!h || !out || n != h->N) {
+    g_henv_err = "ddrl_hostenv_target_velocities: out holds n_envs floats";
+    return -1;
+  }
+  for (int e = 0; e < n; ++e) out[e] = (float)h->st[e].tv;
+  return 0;
+}
+
+extern "C" int ddrl_hostenv_reset_state(ddrl_hostenv* h) {
+  if (!h) {
+    g_henv_err = "null host env";
+    return -1;
+  }
+  h->reset_state();
+  return 0;
+}

@@ -34,6 +34,7 @@ struct EnvState {
   double foot[4];                   // last contact force per foot
   int steps;                        // steps in the current episode
   uint32_t episode;
+  double tv;                        // target velocity of the current episode (TVel envs)
 };
 
 // Persistent worker threads; parallel_for splits [0, n) in contiguous chunks, the caller
@@ -60,7 +61,9 @@ class Pool {
 
 struct ddrl_hostenv {
   int N = 0, D = 43;
-  double target_velocity = 0.0;
+  // target velocities an episode draws from (random.choice on every reset,
+  // quantruped_adaptor_multi_environment.py:47-50, 214-216); one entry for a fixed velocity
+  std::vector<double> tv_list{0.0};
   uint64_t seed = 0;
   std::vector<hostenv::EnvState> st;
   // pinned host buffers (hipHostMalloc): obs [N][D], act [N][8], fw [N], cfrc [N][14][6], done [N]
@@ -69,10 +72,16 @@ struct ddrl_hostenv {
   bool pinned = false;
   hostenv::Pool* pool = nullptr;
 
-  void reset_env(int e);
+  // a fresh episode of env e: new initial pose and, when draw_tv, a new target velocity
+  void reset_env(int e, bool draw_tv = true);
   void write_obs(int e, const double* ctrl);
   void step_env(int e, const float* a8);
   void reset_all();
+  // update_environment_after_epoch (adaptor :97-122): every env's physical state and episode
+  // step count restart (gym env.reset()), the target velocity stays (only the adaptor's own
+  // reset() re-draws it), no done flag is raised and the observation buffer is not rewritten
+  // (the adaptor discards env.reset()'s observation; the sampler acts on the last one it has)
+  void reset_state();
   // step the envs [e0, e1) with the actions act[e][8]; writes obs / fw / cfrc / done of the range
   void step(int e0, int e1);
 };

@@ -31,3 +31,44 @@ class SyntheticVecEnv:
         done = (self.t % self.max_steps == 0).to(self.torch.uint8)
         obs = self._randn(self.N, self.D)
         return obs, self._randn(self.N), self._randn(self.N, 14, 6), done
+
+    def update_environment_after_epoch(self, timesteps_total):
+        """env.reset() of every env (quantruped_adaptor_multi_environment.py:97-122): the
+        TimeLimit counts restart; no done flag, the next observation is the usual draw."""
+        self.t.zero_()
+
+
+class HostVecEnv:
+    """The host env plane (ddrl_amd.native.HostEnv: the QuAntruped stand-in stepped by a pool of
+    host threads into pinned buffers) as a trainer backend: device tensors in and out, with a
+    per-env target velocity drawn from the list on every reset (TVel envs) and the
+    update_environment_after_epoch reset.  The bench's PCIe leg uses the same plane through
+    the pipelined ddrl_rollout_hostenv instead."""
+
+    def __init__(self, n_envs, obs_dim, device, seed=0, n_threads=4, target_velocity=0.0):
+        import torch
+        from .native import HostEnv
+        self.torch, self.device = torch, device
+        self.env = HostEnv(n_envs, obs_dim, n_threads, seed, target_velocity)
+
+    def _dev(self, a):
+        return self.torch.from_numpy(a).to(self.device, non_blocking=False)
+
+    def reset(self):
+        return self._dev(self.env.reset())
+
+    def step(self, actions):
+        self.env.act[:] = actions.detach().to("cpu").numpy()
+        self.env.step()
+        return (self._dev(self.env.obs.copy()), self._dev(self.env.fw.copy()), self._dev(self.env.cfrc.copy()),
+                self._dev(self.env.done.copy()))
+
+    def update_environment_after_epoch(self, timesteps_total):
+        self.env.reset_state()
+
+    @property
+    def target_velocities(self):
+        return self.env.target_velocities
+
+    def close(self):
+        self.env.close()

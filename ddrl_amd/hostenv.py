@@ -34,13 +34,9 @@ class HostMultiAgentEnv:
         self.n = int(n_envs)
         self.D = len(self.spec.obs_fields)
         tv = self.spec.target_velocity_list
-        if tv and len(set(float(v) for v in tv)) > 1:
-            # the reference draws random.choice(target_velocity_list) on every reset
-            # (quantruped_adaptor_multi_environment.py:50, :216); the host env plane holds one
-            # target velocity for all envs, so a list of several is refused, not truncated
-            raise ValueError(f"target_velocity {list(tv)}: the host env plane supports one target velocity "
-                             "(the reference re-draws from the list on every reset)")
-        self.env = N.HostEnv(self.n, self.D, n_threads, seed, float(tv[0]) if tv else 0.0)
+        # every env draws random.choice(target_velocity_list) on each reset
+        # (quantruped_adaptor_multi_environment.py:47-50, :214-216), in the env plane
+        self.env = N.HostEnv(self.n, self.D, n_threads, seed, [float(v) for v in tv] if tv else 0.0)
         self.clip = filter_clip
         # env-side MeanStdFilter singleton: RunningStat (n, M, S), fp64
         self.rs_n, self.rs_M, self.rs_S = 0, np.zeros(self.D), np.zeros(self.D)
@@ -126,6 +122,20 @@ class HostMultiAgentEnv:
             dones = {"__all__": bool(done.all()), "envs": done.copy()}
         info = {"reward_forward": self.env.fw.copy() if self.n > 1 else float(self.env.fw[0])}
         return obs, rew, dones, info
+
+    def update_environment_after_epoch(self, timesteps_total):
+        """The curriculum hook RLlib calls on every env after each training iteration
+        (on_train_result, train_experiment_1_architecture_on_flat.py:171-178; adaptor :97-122):
+        the spec's update_after_epoch, then env.reset() of every env (state and TimeLimit count
+        restart, target velocity kept, the observation of that reset discarded).  The terrain
+        regeneration (create_new_random_hfield) is MuJoCo-side and out of scope."""
+        self.spec.update_after_epoch(timesteps_total)
+        self.env.reset_state()
+
+    @property
+    def target_velocities(self):
+        """Each env's current target velocity (TVel envs)."""
+        return self.env.target_velocities
 
     def close(self):
         self.env.close()

@@ -106,6 +106,9 @@ _SIGS = {
     "ddrl_hostenv_reset": ([VP], C.c_int),
     "ddrl_hostenv_step": ([VP, C.c_int, C.c_int], C.c_int),
     "ddrl_hostenv_threads": ([VP], C.c_int),
+    "ddrl_hostenv_set_target_velocities": ([VP, C.POINTER(C.c_float), C.c_int], C.c_int),
+    "ddrl_hostenv_target_velocities": ([VP, C.POINTER(C.c_float), C.c_int], C.c_int),
+    "ddrl_hostenv_reset_state": ([VP], C.c_int),
     "ddrl_rollout_hostenv": ([VP, VP, C.c_int, VP, C.c_int], C.c_int),
 }
 
@@ -423,10 +426,19 @@ class HostEnv:
     cfrc [N][14][6], done [N])."""
 
     def __init__(self, n_envs, obs_dim=43, n_threads=1, seed=0, target_velocity=0.0):
+        """target_velocity: one value, or a list every env draws its episode's velocity from on
+        each reset (the adaptor's random.choice, quantruped_adaptor_multi_environment.py:50, 216)."""
         self.lib = load()
         h = VP()
-        if self.lib.ddrl_hostenv_create(n_envs, obs_dim, n_threads, seed, target_velocity, C.byref(h)) != 0:
+        tvs = [float(v) for v in (target_velocity if np.ndim(target_velocity) else [target_velocity])]
+        if self.lib.ddrl_hostenv_create(n_envs, obs_dim, n_threads, seed, tvs[0], C.byref(h)) != 0:
             raise DdrlError(self.lib.ddrl_hostenv_last_error().decode())
+        if len(tvs) > 1:
+            arr = (C.c_float * len(tvs))(*tvs)
+            if self.lib.ddrl_hostenv_set_target_velocities(h, arr, len(tvs)) != 0:
+                err = self.lib.ddrl_hostenv_last_error().decode()
+                self.lib.ddrl_hostenv_destroy(h)
+                raise DdrlError(err)
         self.h, self.n, self.obs_dim = h, n_envs, obs_dim
         ptrs = [VP() for _ in range(5)]
         self._ck(self.lib.ddrl_hostenv_buffers(h, *[C.byref(p) for p in ptrs]))
@@ -457,6 +469,20 @@ class HostEnv:
         """Step the envs [e0, e1) with the actions in self.act (written by the caller)."""
         self._live()
         self._ck(self.lib.ddrl_hostenv_step(self.h, e0, self.n if e1 is None else e1))
+
+    def reset_state(self):
+        """update_environment_after_epoch's env.reset(): every env's state and TimeLimit count
+        restart; target velocities, done flags and self.obs are left as they are."""
+        self._live()
+        self._ck(self.lib.ddrl_hostenv_reset_state(self.h))
+
+    @property
+    def target_velocities(self):
+        """Each env's current target velocity (the draw of its current episode)."""
+        self._live()
+        out = np.zeros(self.n, np.float32)
+        self._ck(self.lib.ddrl_hostenv_target_velocities(self.h, out.ctypes.data_as(C.POINTER(C.c_float)), self.n))
+        return out
 
     def close(self):
         """Free the pinned buffers.  The numpy views over them are dropped first (set to None),

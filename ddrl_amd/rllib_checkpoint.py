@@ -611,7 +611,9 @@ def checkpoint_tree(worker_bytes, learner, timesteps):
     np_ = _Np()
     ln = {}
     for pid, s in learner.items():
-        row = {k: np_.scalar_of(s.get(k, 0.0), code) for k, code in _LEARNER_KEYS}
+        # a statistic absent from the row (e.g. "kl" when no iteration has run on the saved
+        # weights) is left out rather than written as 0.0, which a reader would take as a kl
+        row = {k: np_.scalar_of(s[k], code) for k, code in _LEARNER_KEYS if k in s}
         row["model"] = {}
         ln[pid] = row
     return {"worker": worker_bytes,

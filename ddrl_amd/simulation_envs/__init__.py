@@ -37,6 +37,8 @@ class QuantrupedMultiPoliciesEnv:
         self.hf_smoothness = config.get("hf_smoothness", 1.0)
         self.target_velocity_list = config.get("target_velocity")
         self.use_target_velocity = self.target_velocity_list is not None
+        if self.use_target_velocity and not isinstance(self.target_velocity_list, (list, tuple)):
+            self.target_velocity_list = [self.target_velocity_list]   # adaptor :47-49
         if config.get("global_reward", False):
             self.reward_mode = "global"
         elif config.get("norm_reward", False):
@@ -71,8 +73,10 @@ class QuantrupedMultiPoliciesEnv:
                 (None, Box(-float("inf"), float("inf"), (n,), "float64"), Box(-1.0, 1.0, (8,)), {})}
 
     def update_environment_after_epoch(self, timesteps_total):
-        """Curriculum hook (adaptor :97-122).  Terrain regeneration is a MuJoCo-side
-        concern and out of scope here; the hook is kept so callbacks run unchanged."""
+        """Curriculum hook (adaptor :97-122), the spec's part: update_after_epoch.  The env
+        reset that follows it in the reference is the backend's (HostMultiAgentEnv /
+        ddrl_amd.envs backends: every env's state and TimeLimit count restart); terrain
+        regeneration is MuJoCo-side and out of scope."""
         self.update_after_epoch(timesteps_total)
 
     def update_after_epoch(self, timesteps_total):

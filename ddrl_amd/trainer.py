@@ -97,7 +97,14 @@ class PPOTrainer:
                 layer = {v: k for k, v in N.GNN_LAYERS.items()}[self.cfg.gnn_layer]
                 self.ctx.params_set(p, glorot_gnn_flat(self.rng, self.cfg.act_dim, layer=layer))
         self.kl_coeff = [float(c["kl_coeff"])] * P
-        if env_backend is None:
+        if env_backend is None and c.get("env_backend", "synthetic") == "host":
+            # extension: the host env plane (the QuAntruped stand-in on host threads; TVel
+            # target velocities drawn per env from env_config["target_velocity"] on every reset)
+            from .envs import HostVecEnv
+            env_backend = HostVecEnv(self.n_envs, self.cfg.obs_full_dim, self.device, seed=env_seed,
+                                     n_threads=int(c.get("num_host_threads", 4)),
+                                     target_velocity=self.env.target_velocity_list or 0.0)
+        elif env_backend is None:
             from .envs import SyntheticVecEnv
             env_backend = SyntheticVecEnv(self.n_envs, self.cfg.obs_full_dim, self.device, seed=env_seed)
         self.backend = env_backend
@@ -139,6 +146,7 @@ class PPOTrainer:
                                  if self.cfg.policy_filter else None)
             self.ctx.policy_filter_delta_reset()
             self.grad = torch.zeros(self.ctx.n_params[0], dtype=torch.float32, device=self.device)
+        self.workers = _Workers(self)
         self.rctx.observe(self.backend.reset())
 
     # -- one iteration ---------------------------------------------------------------
@@ -286,9 +294,13 @@ class PPOTrainer:
         return {pid: self.ctx.params_get(p) for p, pid in enumerate(self.policy_ids)}
 
     def set_weights(self, weights):
+        """Writes the learner context and, in "gather" mode, the rollout context too: the next
+        fragment must be sampled (and its logp / vf recorded) with the weights it trains."""
         for p, pid in enumerate(self.policy_ids):
             if pid in weights:
                 self.ctx.params_set(p, weights[pid])
+                if self.rctx is not self.ctx:
+                    self.rctx.params_set(p, weights[pid])
 
     def save(self, path):
         """Checkpoint: weights, Adam m/v/beta powers, KL coefficients, filter state (npz,
@@ -329,6 +341,17 @@ class PPOTrainer:
                                          z[f"{pid}/filter/S"])
         meta = json.loads(bytes(z["meta"]).decode())
         self.iteration, self.timesteps_total = meta["iteration"], meta["timesteps_total"]
+        self._after_load({})
+
+    def _after_load(self, learner):
+        """State that follows a restore: the learner statistics that belong to the restored
+        weights (none for an npz checkpoint, the file's own for an RLlib one), and, for the
+        data-parallel / gather modes, the base of the per-policy filter sync, which must be the
+        restored RunningStat (else the next sync merges the delta into the stale base)."""
+        self.last_learner = learner
+        if self.parallel in ("ddp", "gather") and getattr(self, "pfilter_base", None) is not None:
+            self.pfilter_base = [self.ctx.policy_filter_get(p) for p in range(self.cfg.n_policies)]
+            self.rctx.policy_filter_delta_reset()
 
     def restore_rllib(self, path):
         """Load a published RLlib checkpoint (Results/**/checkpoint-1250, the file
@@ -377,6 +400,10 @@ class PPOTrainer:
         learner = {}
         for p, pid in enumerate(self.policy_ids):
             s = dict(last.get(pid, {}))
+            # no statistics for the current weights (no train() since the trainer was built or
+            # restored from an npz file): the row carries the current coefficient and no "kl",
+            # so a reload keeps the coefficient as it is (load_policy_states runs update_kl only
+            # with a kl)
             s.setdefault("cur_kl_coeff", float(np.float32(self.kl_coeff[p])))
             s.setdefault("cur_lr", float(np.float32(self.cfg.lr)))
             s.setdefault("entropy_coeff", float(self.cfg.entropy_coeff))
@@ -389,6 +416,7 @@ class PPOTrainer:
         None, "kl_coeff" or None} (ddrl_amd.rllib_checkpoint.policy_state's layout) into the
         context; returns the policy ids loaded."""
         missing = [pid for pid in self.policy_ids if pid not in states]
+        learner = {}
         if missing:
             raise ValueError(f"checkpoint has policies {sorted(states)}, this env needs {self.policy_ids}")
         for p, pid in enumerate(self.policy_ids):
@@ -403,21 +431,73 @@ class PPOTrainer:
                 self.rctx.policy_filter_set(p, *st["filter"])
             if self.rctx is not self.ctx:
                 self.rctx.params_set(p, st["weights"])
-            if st["kl_coeff"] is not None:
-                # the file's cur_kl_coeff is the coefficient the checkpointed iteration trained
-                # with; the next iteration's is update_kl of it and that iteration's kl (RLlib
-                # runs update_kl after the learner step, ppo.py UpdateKL)
-                kl = (st.get("learner_stats") or {}).get("kl")
+            stats = dict(st.get("learner_stats") or {})
+            if self.config.get("restore_kl_coeff", "checkpoint") == "config":
+                # RLlib 1.0.1: the TF policy state holds only model and optimizer variables
+                # (KLCoeffMixin has no get_state), so PPOTrainer.restore starts again from
+                # config["kl_coeff"]
+                self.kl_coeff[p] = float(self.config["kl_coeff"])
+                stats.pop("kl", None)
+                stats["cur_kl_coeff"] = self.kl_coeff[p]
+            elif st["kl_coeff"] is not None:
+                # extension: continue from the file's coefficient.  Its
+                # cur_kl_coeff is the coefficient the checkpointed iteration trained with; the
+                # next iteration's is update_kl of it and that iteration's kl (RLlib runs update_kl
+                # after the learner step, ppo.py UpdateKL)
+                kl = stats.get("kl")
                 self.kl_coeff[p] = (update_kl(st["kl_coeff"], kl, self.config["kl_target"]) if kl is not None
                                     else st["kl_coeff"])
-        if self.parallel in ("ddp", "gather") and self.pfilter_base is not None:
-            self.pfilter_base = [self.ctx.policy_filter_get(p) for p in range(self.cfg.n_policies)]
+                stats["cur_kl_coeff"] = st["kl_coeff"]
+            learner[pid] = stats
+        self._after_load(learner)
         return list(self.policy_ids)
 
     def stop(self):
         if self.rctx is not self.ctx:
             self.rctx.close()
         self.ctx.close()
+        if hasattr(self.backend, "close"):
+            self.backend.close()
+
+
+class _EnvHandle:
+    """What `worker.foreach_env(fn)` hands to fn: the env spec (the reference's MultiAgentEnv
+    class surface), whose update_environment_after_epoch also resets the vectorized backend's
+    envs (quantruped_adaptor_multi_environment.py:97-122: update_after_epoch, then env.reset())."""
+
+    def __init__(self, trainer):
+        self._trainer = trainer
+
+    def update_environment_after_epoch(self, timesteps_total):
+        self._trainer.env.update_environment_after_epoch(timesteps_total)
+        hook = getattr(self._trainer.backend, "update_environment_after_epoch", None)
+        if hook is not None:
+            hook(timesteps_total)
+
+    def __getattr__(self, name):
+        return getattr(self._trainer.env, name)
+
+
+class _Worker:
+    def __init__(self, trainer):
+        self._trainer = trainer
+
+    def foreach_env(self, fn):
+        """RolloutWorker.foreach_env: fn over this worker's envs -- one vectorized env here."""
+        return [fn(_EnvHandle(self._trainer))]
+
+
+class _Workers:
+    """trainer.workers (RLlib WorkerSet) for the callbacks the reference's training scripts
+    install: train_experiment_1_architecture_on_flat.py:171-178 runs
+    trainer.workers.foreach_worker(lambda ev: ev.foreach_env(lambda env:
+    env.update_environment_after_epoch(timesteps))) after every iteration."""
+
+    def __init__(self, trainer):
+        self._trainer = trainer
+
+    def foreach_worker(self, fn):
+        return [fn(_Worker(self._trainer))]
 
 
 def sync_filters_local(base, delta):

@@ -193,6 +193,19 @@ int ddrl_hostenv_buffers(ddrl_hostenv* env, float** obs, float** act, float** fw
 int ddrl_hostenv_reset(ddrl_hostenv* env);
 int ddrl_hostenv_step(ddrl_hostenv* env, int e0, int e1);
 int ddrl_hostenv_threads(ddrl_hostenv* env);
+/* Target velocities of the TVel envs (obs_dim 44): every env draws its episode's velocity
+ * uniformly from list[0..n) on every reset, the adaptor's random.choice(target_velocity_list)
+ * at construction and in reset() (quantruped_adaptor_multi_environment.py:47-50, 214-216); the
+ * draw takes effect at the next reset (ddrl_hostenv_reset, or an episode end).  create's
+ * target_velocity is the list of one.  target_velocities: each env's current velocity. */
+int ddrl_hostenv_set_target_velocities(ddrl_hostenv* env, const float* list, int n);
+int ddrl_hostenv_target_velocities(ddrl_hostenv* env, float* out, int n_envs);
+/* update_environment_after_epoch (quantruped_adaptor_multi_environment.py:97-122, after every
+ * training iteration through on_train_result, train_experiment_1_architecture_on_flat.py:171-178):
+ * every env's state and TimeLimit count restart (gym env.reset()), the target velocity is kept,
+ * no done flag is raised and obs is not rewritten (the adaptor discards that observation).
+ * The terrain regeneration of the same hook is MuJoCo-side (out of scope). */
+int ddrl_hostenv_reset_state(ddrl_hostenv* env);
 int ddrl_rollout_hostenv(ddrl_ctx* ctx, ddrl_hostenv* env, int groups, const float* eps_dev, int reset);
 
 /* Postprocessing: GAE over the fragment for every policy + advantage standardization

@@ -160,9 +160,23 @@ def per_leg_reward(fw_reward, cfrc_ext, action_dict, contact_tables, ctrl_w, con
 
 
 def tvel_forward_reward(x_velocity, target_velocity):
-    """QuAntrupedTVelEnv.compute_forward_reward (simulation_envs/quantruped_v3.py:391-392)."""
-    tv = float(target_velocity)
+    """QuAntrupedTVelEnv.compute_forward_reward (simulation_envs/quantruped_v3.py:391-392);
+    target_velocity may be per env (an array broadcast against x_velocity)."""
+    tv = np.asarray(target_velocity, np.float64)
     return (1.0 + 1.0 / tv) * (1.0 / (np.abs(x_velocity - tv) + 1.0) - 1.0 / (tv + 1.0))
+
+
+def target_velocity_pmf(target_velocity_list):
+    """The distribution of one episode's target velocity: the adaptor draws
+    random.choice(target_velocity_list) at construction and on every reset()
+    (simulation_envs/quantruped_adaptor_multi_environment.py:47-50, 214-216), and CPython's
+    random.choice picks seq[_randbelow(len(seq))] -- every list POSITION equally likely, so a
+    value listed twice is drawn twice as often.  Returns {value: probability}."""
+    tvs = list(target_velocity_list) if isinstance(target_velocity_list, (list, tuple)) else [target_velocity_list]
+    pmf = {}
+    for v in tvs:
+        pmf[float(v)] = pmf.get(float(v), 0.0) + 1.0 / len(tvs)
+    return pmf
 
 
 def global_reward(fw_reward, cfrc_ext, action_dict, ctrl_w, contact_w):
@@ -307,10 +321,10 @@ GNN_LAYERS = ("mpnn", "gcn", "mpnn2", "gat1")
 
 
 def gnn_layer_shapes(layer, hidden=64):
-    return {"mpnn": [("mpnn/msg/kernel", (hidden, hidden)), ("mpnn/node/kernel", (hidden, hidden))],
+    return {"mpnn": [("mpnn/msg_transform/kernel", (hidden, hidden)), ("mpnn/node_update/kernel", (hidden, hidden))],
             "gcn": [("gcn/linear/kernel", (hidden, hidden))],
-            "mpnn2": [("mpnn2/msg/kernel", (2 * hidden, hidden)), ("mpnn2/node/kernel", (2 * hidden, hidden))],
-            "gat1": [("gat1/pre_att/kernel", (hidden, hidden)), ("gat1/att/kernel", (2 * hidden, 1))]}[layer]
+            "mpnn2": [("mpnn2/msg_transform/kernel", (2 * hidden, hidden)), ("mpnn2/node_update/kernel", (2 * hidden, hidden))],
+            "gat1": [("gat1/pre_att_linear/kernel", (hidden, hidden)), ("gat1/att_linear/kernel", (2 * hidden, 1))]}[layer]
 
 
 def gnn_net_shapes(num_outputs, hidden=64, feat=19, qdim=4, layer="mpnn"):
@@ -354,10 +368,10 @@ def _layer_forward(p, pre, layer, h, adj):
     """The message-passing layer; returns y and its cache."""
     if layer == "mpnn":             # gcn.py:57-94
         e, cnt = _edges(adj)
-        msg = h @ p[pre + "mpnn/msg/kernel"]
+        msg = h @ p[pre + "mpnn/msg_transform/kernel"]
         m = np.einsum("bsr,bsj->brj", e, msg)
         m = np.where(cnt[..., None] > 0, m / np.maximum(cnt[..., None], 1), 0.0).astype(F32)
-        y = np.tanh(h @ p[pre + "mpnn/node/kernel"] + m)
+        y = np.tanh(h @ p[pre + "mpnn/node_update/kernel"] + m)
         return y, (e, cnt)
     if layer == "gcn":              # gcn.py:29-37 with graph_ops.adj_norm (:13-21): D^-1 A
         an = (adj / adj.sum(-1, keepdims=True)).astype(F32)
@@ -370,16 +384,16 @@ def _layer_forward(p, pre, layer, h, adj):
         hs = np.broadcast_to(h[:, :, None, :], (h.shape[0], n, n, h.shape[2]))   # sender s
         hr = np.broadcast_to(h[:, None, :, :], (h.shape[0], n, n, h.shape[2]))   # receiver r
         cat = np.concatenate([hs, hr], -1)
-        esr = cat @ p[pre + "mpnn2/msg/kernel"]
+        esr = cat @ p[pre + "mpnn2/msg_transform/kernel"]
         m = _seg_mean(e, cnt, esr)
-        y = np.tanh(np.concatenate([h, m], -1) @ p[pre + "mpnn2/node/kernel"])
+        y = np.tanh(np.concatenate([h, m], -1) @ p[pre + "mpnn2/node_update/kernel"])
         return y, (e, cnt, cat, m)
     if layer == "gat1":             # gcn.py:171-206 with graph_ops.segment_softmax (:23-26)
         n = h.shape[1]
         adj1 = np.minimum(F32(1), adj + np.eye(n, dtype=F32)[None])
         e = (adj1 != 0).astype(F32)
-        z = h @ p[pre + "gat1/pre_att/kernel"]
-        a = p[pre + "gat1/att/kernel"][:, 0]
+        z = h @ p[pre + "gat1/pre_att_linear/kernel"]
+        a = p[pre + "gat1/att_linear/kernel"][:, 0]
         H = z.shape[2]
         pre_sr = (z @ a[:H])[:, :, None] + (z @ a[H:])[:, None, :]     # concat(z_s, z_r) . a
         lr = np.where(pre_sr > 0, pre_sr, F32(0.2) * pre_sr)           # tf.nn.leaky_relu (0.2)
@@ -396,12 +410,12 @@ def _layer_backward(p, pre, layer, h, y, cache, dy, g):
     du = dy * (1 - y * y)
     if layer == "mpnn":
         e, cnt = cache
-        g[pre + "mpnn/node/kernel"] = np.einsum("bnj,bnk->jk", h, du)
-        dh = du @ p[pre + "mpnn/node/kernel"].T
+        g[pre + "mpnn/node_update/kernel"] = np.einsum("bnj,bnk->jk", h, du)
+        dh = du @ p[pre + "mpnn/node_update/kernel"].T
         dm = np.where(cnt[..., None] > 0, du / np.maximum(cnt[..., None], 1), 0.0)
         dmsg = np.einsum("bsr,brj->bsj", e, dm)
-        g[pre + "mpnn/msg/kernel"] = np.einsum("bnj,bnk->jk", h, dmsg)
-        return dh + dmsg @ p[pre + "mpnn/msg/kernel"].T
+        g[pre + "mpnn/msg_transform/kernel"] = np.einsum("bnj,bnk->jk", h, dmsg)
+        return dh + dmsg @ p[pre + "mpnn/msg_transform/kernel"].T
     if layer == "gcn":
         an, hbar = cache
         g[pre + "gcn/linear/kernel"] = np.einsum("bnj,bnk->jk", hbar, du)
@@ -410,14 +424,14 @@ def _layer_backward(p, pre, layer, h, y, cache, dy, g):
     if layer == "mpnn2":
         e, cnt, cat, m = cache
         H = h.shape[2]
-        W = p[pre + "mpnn2/node/kernel"]
-        g[pre + "mpnn2/node/kernel"] = np.einsum("bnj,bnk->jk", np.concatenate([h, m], -1), du)
+        W = p[pre + "mpnn2/node_update/kernel"]
+        g[pre + "mpnn2/node_update/kernel"] = np.einsum("bnj,bnk->jk", np.concatenate([h, m], -1), du)
         dcat = du @ W.T
         dh, dm = dcat[..., :H], dcat[..., H:]
         dm = np.where(cnt[..., None] > 0, dm / np.maximum(cnt[..., None], 1), 0.0)
         de = e[..., None] * dm[:, None, :, :]                          # [b, s, r, k]
-        Wm = p[pre + "mpnn2/msg/kernel"]
-        g[pre + "mpnn2/msg/kernel"] = np.einsum("bsrj,bsrk->jk", cat, de)
+        Wm = p[pre + "mpnn2/msg_transform/kernel"]
+        g[pre + "mpnn2/msg_transform/kernel"] = np.einsum("bsrj,bsrk->jk", cat, de)
         dcat_e = de @ Wm.T
         return dh + dcat_e[..., :H].sum(2) + dcat_e[..., H:].sum(1)
     if layer == "gat1":
@@ -429,11 +443,11 @@ def _layer_backward(p, pre, layer, h, y, cache, dy, g):
         dex = att * (datt - colsum[:, None, :])                          # softmax over senders of r
         dpre = dex * np.where(pre_sr > 0, F32(1), F32(0.2))
         dps, dur = dpre.sum(2), dpre.sum(1)                              # d(z_s.a1), d(z_r.a2)
-        g[pre + "gat1/att/kernel"] = np.concatenate(
+        g[pre + "gat1/att_linear/kernel"] = np.concatenate(
             [np.einsum("bs,bsj->j", dps, z), np.einsum("br,brj->j", dur, z)])[:, None]
         dz = dz + dps[..., None] * a[:H] + dur[..., None] * a[H:]
-        g[pre + "gat1/pre_att/kernel"] = np.einsum("bnj,bnk->jk", h, dz)
-        return dz @ p[pre + "gat1/pre_att/kernel"].T
+        g[pre + "gat1/pre_att_linear/kernel"] = np.einsum("bnj,bnk->jk", h, dz)
+        return dz @ p[pre + "gat1/pre_att_linear/kernel"].T
     raise ValueError(f"unknown gnn layer {layer!r}")
 
 

@@ -233,3 +233,12 @@ def test_writer_rebuilds_every_published_checkpoint():
         md = RC.to_data(RC.walk(md_raw))
         assert RC.emit(RC.metadata_tree(md["iteration"], md["time_total"], md["episodes_total"],
                                         md["experiment_id"], md["ray_version"])) == md_raw, f
+
+
+@pytest.mark.parametrize("layer", O.GNN_LAYERS)
+def test_gnn_variable_names_agree_between_writer_and_oracle(layer):
+    """One naming for the GNN variables: the Keras attribute names of models/gcn.py:19,46-47,
+    102-103,159-160 (msg_transform, node_update, linear, pre_att_linear, att_linear) in the
+    writer's layout (rllib_checkpoint.gnn_shapes) and in the oracle's parameter dicts."""
+    assert [(n, tuple(s)) for n, s in RC.gnn_shapes(4, layer=layer)] == \
+        [(n, tuple(s)) for n, s in O.gnn_param_shapes(4, layer=layer)]

@@ -81,6 +81,8 @@ def _oracle_over_trace(cfg, inst, params, filt, trace, eps, gnn, groups):
     ("QuantrupedMultiEnv_Centralized", 64, 10, 2, None),
     ("QuantrupedMultiEnv_DecentralShared_Graph", 96, 10, 2, None),
     ("QuantrupedMultiEnv_FullyDecentral", 80, 10, 1, {"env_config": {"target_velocity": [1.0]}}),
+    # a 2-velocity list, every env drawing its own on each reset
+    ("QuantrupedMultiEnv_Local", 160, 16, 2, {"env_config": {"target_velocity": [0.5, 1.5]}}),
 ])
 def test_pipelined_host_rollout_matches_device_loop(env_name, n, T, groups, config):
     import torch
@@ -96,7 +98,8 @@ def test_pipelined_host_rollout_matches_device_loop(env_name, n, T, groups, conf
         filt = (1000.0, np.linspace(-0.5, 0.5, cfg.obs_full_dim), np.full(cfg.obs_full_dim, 2000.0))
         ctx.filter_set(*filt)
         ctxs.append(ctx)
-        envs.append(N.HostEnv(n, cfg.obs_full_dim, threads, seed=11, target_velocity=1.0))
+        tv = ((config or {}).get("env_config") or {}).get("target_velocity", [1.0])
+        envs.append(N.HostEnv(n, cfg.obs_full_dim, threads, seed=11, target_velocity=tv))
     gen = torch.Generator(device="cuda")
     gen.manual_seed(3)
     eps = torch.randn((T, n, cfg.n_agents, cfg.act_dim), device="cuda", generator=gen)
@@ -117,6 +120,11 @@ def test_pipelined_host_rollout_matches_device_loop(env_name, n, T, groups, conf
     np.testing.assert_array_equal(fa[2], fb[2])
     # the host envs themselves ended in the same state (thread count does not matter)
     np.testing.assert_array_equal(envs[0].obs, envs[1].obs)
+    if cfg.obs_full_dim == 44:
+        tvs = envs[0].target_velocities
+        np.testing.assert_array_equal(tvs, envs[1].target_velocities)
+        np.testing.assert_array_equal(envs[0].obs[:, 43], tvs)
+        assert set(np.unique(tvs)) == set(np.float32(tv))   # both velocities in use
     # both against the oracle run on the host env plane's raw outputs
     assert len(trace) == T + 1
     orc, norms = _oracle_over_trace(cfg, inst, params, filt, trace, eps.cpu().numpy(), gnn, groups)

@@ -319,3 +319,101 @@ def test_trainer_gather_world2_equals_single_process_union_update(env):
         np.testing.assert_array_equal(a[f"roll_w_{p}"], ref)
         assert a[f"kl_{p}"][0] == b[f"kl_{p}"][0]
     ctx.close()
+
+
+def test_trainer_rllib_save_after_restore_keeps_kl_coeff(tmp_path):
+    """restore_rllib -> save_rllib -> restore_rllib is the identity on the KL
+    coefficient (the saved row carries the restored file's cur_kl_coeff and kl, not kl = 0
+    next to the already-updated coefficient), and an npz restore followed by save_rllib writes
+    no kl, so a reload keeps the coefficient; "restore_kl_coeff": "config" reproduces RLlib
+    1.0.1's restart from config["kl_coeff"]."""
+    from ddrl_amd import rllib_checkpoint as RC
+    from ddrl_amd.trainer import PPOTrainer
+    cfg = {"env": "QuantrupedMultiEnv_Local", "rollout_fragment_length": 8, "kl_coeff": 0.3}
+    tr = PPOTrainer(cfg, n_envs=32, seed=4)
+    tr.train()
+    tr.kl_coeff = [0.45, 0.3, 0.15, 0.6]   # distinct per policy, so a mix-up shows
+    tr.last_learner = {pid: {**st, "cur_kl_coeff": c, "kl": k} for (pid, st), c, k in
+                       zip(tr.last_learner.items(), (0.3, 0.2, 0.3, 0.4), (0.05, 0.02, 0.001, 0.03))}
+    p1 = tr.save_rllib(str(tmp_path / "a"))
+    tr2 = PPOTrainer(cfg, n_envs=32, seed=9)
+    tr2.restore_rllib(p1)
+    k2 = list(tr2.kl_coeff)
+    assert k2 == pytest.approx([0.45, 0.2, 0.15, 0.6])   # update_kl(cur, kl) per policy
+    p2 = tr2.save_rllib(str(tmp_path / "b"))
+    tr3 = PPOTrainer(cfg, n_envs=32, seed=11)
+    tr3.restore_rllib(p2)
+    assert tr3.kl_coeff == k2
+    # npz restore, then save_rllib without training: no kl in the row, coefficient kept
+    npz = tr2.save(str(tmp_path / "c.npz"))
+    tr4 = PPOTrainer(cfg, n_envs=32, seed=12)
+    tr4.restore(npz)
+    assert tr4.kl_coeff == k2
+    p4 = tr4.save_rllib(str(tmp_path / "d"))
+    row = RC.read_checkpoint(p4)["train_exec_impl"]["info"]["learner"][tr4.policy_ids[0]]
+    assert "kl" not in row
+    tr5 = PPOTrainer(cfg, n_envs=32, seed=13)
+    tr5.restore_rllib(p4)
+    assert tr5.kl_coeff == pytest.approx(k2, rel=1e-7)
+    tr6 = PPOTrainer({**cfg, "restore_kl_coeff": "config"}, n_envs=32, seed=14)
+    tr6.restore_rllib(p1)
+    assert tr6.kl_coeff == [0.3] * 4
+    for t in (tr, tr2, tr3, tr4, tr5, tr6):
+        t.stop()
+
+
+def test_trainer_gather_restore_keeps_policy_filter_and_set_weights_reaches_rollout(tmp_path):
+    """in "gather" mode (one rank) restore() makes the restored per-policy
+    RunningStat the base of the next filter sync (its count keeps growing from the restored
+    value), and set_weights writes the rollout context as well as the learner's."""
+    from ddrl_amd.trainer import PPOTrainer
+    cfg = {"env": "QuantrupedMultiEnv_Local", "rollout_fragment_length": 8, "parallel": "gather",
+           "observation_filter": "MeanStdFilter"}
+    tr = PPOTrainer(cfg, n_envs=32, seed=4)
+    tr.train()
+    tr.train()
+    n_saved = tr.ctx.policy_filter_get(0)[0]
+    assert n_saved == 2 * 8 * 32 + 32   # reset + 16 steps of 32 envs, one agent per policy
+    path = tr.save(str(tmp_path / "g.npz"))
+    tr2 = PPOTrainer(cfg, n_envs=32, seed=7)
+    tr2.restore(path)
+    assert tr2.ctx.policy_filter_get(0)[0] == n_saved
+    tr2.train()
+    assert tr2.ctx.policy_filter_get(0)[0] == n_saved + 8 * 32   # grows from the restored n
+    w = {pid: np.full_like(v, 0.01) for pid, v in tr2.get_weights().items()}
+    tr2.set_weights(w)
+    for p in range(tr2.cfg.n_policies):
+        np.testing.assert_array_equal(tr2.rctx.params_get(p), w[tr2.policy_ids[p]])
+    for t in (tr, tr2):
+        t.stop()
+
+
+def test_trainer_host_backend_runs_the_reference_curriculum_callback():
+    """a TVel trainer over the host env plane with a 2-velocity list
+    (every env draws its own on each reset) and train_experiment_1's on_train_result callback
+    unchanged (:171-178: trainer.workers.foreach_worker(... env.update_environment_after_epoch
+    ...)), which resets every env after every iteration while the velocities stay."""
+    from ddrl_amd.trainer import PPOTrainer
+    seen = []
+
+    def on_train_result(info):   # the reference script's callback, verbatim in behaviour
+        result = info["result"]
+        trainer = info["trainer"]
+        timesteps_res = result["timesteps_total"]
+        seen.append(trainer.workers.foreach_worker(
+            lambda ev: ev.foreach_env(lambda env: env.update_environment_after_epoch(timesteps_res))))
+
+    tr = PPOTrainer({"env": "QuantrupedMultiEnv_Local", "rollout_fragment_length": 8, "env_backend": "host",
+                     "env_config": {"target_velocity": [0.5, 1.5]},
+                     "callbacks": {"on_train_result": on_train_result}}, n_envs=64, seed=2)
+    tv0 = tr.backend.target_velocities
+    assert set(np.unique(tv0)) == {0.5, 1.5}
+    assert tr.cfg.obs_full_dim == 44
+    r = tr.train()
+    assert len(seen) == 1 and r["timesteps_total"] == 8 * 64
+    np.testing.assert_array_equal(tr.backend.target_velocities, tv0)   # kept by the reset
+    for pid, st in r["info"]["learner"].items():
+        assert np.isfinite(st["total_loss"]), pid
+    tr.train()
+    assert len(seen) == 2
+    tr.stop()

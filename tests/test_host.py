@@ -301,15 +301,95 @@ def test_host_env_close_drops_buffer_views_and_reset_returns_copy():
     assert np.isfinite(o).all()              # the caller's copy stays valid
 
 
-def test_host_dict_env_refuses_several_target_velocities():
-    """the reference re-draws random.choice(target_velocity_list) on every reset
-    (quantruped_adaptor_multi_environment.py:50, :216); the host env plane holds one target
-    velocity, so a list of several distinct values is refused rather than silently truncated."""
+def test_host_env_draws_target_velocity_per_reset_like_random_choice():
+    """VERDICT r3 missing 2: every env draws its episode's target velocity from the list on each
+    reset (random.choice, quantruped_adaptor_multi_environment.py:47-50, 214-216).  Over all
+    episodes (the reset of every env, then every episode end) the draws follow the oracle's
+    rule (every list position equally likely: oracle.target_velocity_pmf) by a chi-square test;
+    a velocity changes only at an episode end; the TVel observation column and the forward
+    reward use the env's own velocity (the reward against the oracle's formula per env, with
+    the plain env's x velocity from a 43-column twin stepped with the same actions)."""
+    from scipy import stats
+    from oracle import ddrl_oracle as O
+    tv_list = [0.5, 1.0, 1.0, 2.0]
+    n = 192
+    twin = N.HostEnv(n, 43, 2, seed=21)
+    env = N.HostEnv(n, 44, 3, seed=21, target_velocity=tv_list)
+    twin.reset()
+    env.reset()
+    tv = env.target_velocities
+    draws = list(tv)
+    assert np.all(env.obs[:, 43] == tv)
+    rng = np.random.default_rng(8)
+    n_done = 0
+    for _ in range(1100):          # past the 1000-step TimeLimit: every env ends an episode
+        a = rng.uniform(-1, 1, size=(n, 8)).astype(np.float32)
+        twin.act[:] = a
+        env.act[:] = a
+        twin.step()
+        env.step()
+        done = env.done.astype(bool)
+        np.testing.assert_array_equal(done, twin.done.astype(bool))
+        np.testing.assert_allclose(env.fw, O.tvel_forward_reward(twin.fw.astype(np.float64), tv),
+                                   rtol=1e-5, atol=1e-6)   # this step's reward: the episode's velocity
+        new = env.target_velocities
+        assert np.all(new[~done] == tv[~done])                  # no re-draw inside an episode
+        draws += list(new[done])
+        n_done += int(done.sum())
+        tv = new
+        assert np.all(env.obs[:, 43] == tv)
+        np.testing.assert_array_equal(env.obs[:, :43], twin.obs)
+    assert n_done >= n
+    pmf = O.target_velocity_pmf(tv_list)
+    vals = sorted(pmf)
+    counts = np.array([np.sum(np.asarray(draws) == np.float32(v)) for v in vals])
+    assert counts.sum() == len(draws)
+    expected = np.array([pmf[v] for v in vals]) * len(draws)
+    assert stats.chisquare(counts, expected).pvalue > 1e-3, (counts, expected)
+    with pytest.raises(N.DdrlError):
+        N.HostEnv(8, 44, 1, target_velocity=[1.0, 0.0])      # the TVel reward divides by it
+    twin.close()
+    env.close()
+
+
+def test_host_env_reset_state_is_update_environment_after_epoch():
+    """VERDICT r3 missing 3: update_environment_after_epoch (adaptor :97-122, run on every env
+    after every iteration by train_experiment_1's on_train_result) resets the gym env: every
+    env's state and TimeLimit count restart, the target velocity stays, no done flag is raised,
+    and the observation buffer is untouched (the adaptor discards that observation).  Every env
+    then runs the full 1000 steps to its TimeLimit (the staggered phases are gone)."""
     from ddrl_amd.hostenv import HostMultiAgentEnv
-    with pytest.raises(ValueError, match="one target velocity"):
-        HostMultiAgentEnv("QuantrupedMultiEnv_Local", {"target_velocity": [0.5, 1.0]})
-    env = HostMultiAgentEnv("QuantrupedMultiEnv_Local", {"target_velocity": [0.75, 0.75]})
-    env.env.close()
+    n = 24
+    env = N.HostEnv(n, 44, 2, seed=4, target_velocity=[0.5, 1.5])
+    env.reset()
+    rng = np.random.default_rng(1)
+    for _ in range(5):
+        env.act[:] = rng.uniform(-1, 1, size=(n, 8)).astype(np.float32)
+        env.step()
+    obs, done, tv = env.obs.copy(), env.done.copy(), env.target_velocities
+    env.reset_state()
+    np.testing.assert_array_equal(env.obs, obs)
+    np.testing.assert_array_equal(env.done, done)
+    np.testing.assert_array_equal(env.target_velocities, tv)
+    env.act[:] = 0.0
+    steps_to_done = np.full(n, -1)
+    for k in range(1, 1001):
+        env.step()
+        d = env.done.astype(bool)
+        steps_to_done[d & (steps_to_done < 0)] = k
+    # with zero actions the stand-in torso stays up: every env reaches the TimeLimit exactly
+    assert np.all(steps_to_done == 1000), steps_to_done
+    env.close()
+    # the dict API forwards the hook
+    denv = HostMultiAgentEnv("QuantrupedMultiEnv_Local", {"target_velocity": [0.5, 1.0]}, n_envs=8, n_threads=2)
+    o = denv.reset()
+    assert set(np.unique(denv.target_velocities)) <= {0.5, 1.0}
+    before = denv.target_velocities
+    denv.update_environment_after_epoch(1000)
+    np.testing.assert_array_equal(denv.target_velocities, before)
+    o2, r, d, _ = denv.step({a: np.zeros((8, 2)) for a in denv.agent_names})
+    assert not d["__all__"] and np.isfinite(o2["agent_FL"]).all()
+    denv.close()
 
 
 def test_gnn_layer_config_is_validated():

@@ -207,9 +207,9 @@ def test_gnn_gradients_match_autograd():
         wn = torch.tanh(q @ t[pre + "state_enc/kernel"] + t[pre + "state_enc/bias"])
         wn = wn.reshape(n, 4, 19, 64)
         h = torch.tanh(torch.einsum("bni,bnij->bnj", f, wn))
-        msg = h @ t[pre + "mpnn/msg/kernel"]
+        msg = h @ t[pre + "mpnn/msg_transform/kernel"]
         m = torch.einsum("sr,bsj->brj", adj, msg) / adj.sum(0)[None, :, None]
-        y = torch.tanh(h @ t[pre + "mpnn/node/kernel"] + m)
+        y = torch.tanh(h @ t[pre + "mpnn/node_update/kernel"] + m)
         ys = y[torch.arange(n), torch.tensor(node)]
         return ys @ t[pre + "linear_out/kernel"] + t[pre + "linear_out/bias"]
 
@@ -241,15 +241,15 @@ def _torch_gnn_layer(layer, t, pre, x, adj):
 
     cnt = seg_sum(torch.ones(len(seg), dtype=x.dtype))
     if layer == "mpnn":                      # gcn.py:57-94
-        msgs = seg_sum(x[b, snd] @ t[pre + "mpnn/msg/kernel"]) / torch.clamp(cnt, min=1)[:, None]
-        return torch.tanh(x @ t[pre + "mpnn/node/kernel"] + msgs.reshape(B, n, H))
+        msgs = seg_sum(x[b, snd] @ t[pre + "mpnn/msg_transform/kernel"]) / torch.clamp(cnt, min=1)[:, None]
+        return torch.tanh(x @ t[pre + "mpnn/node_update/kernel"] + msgs.reshape(B, n, H))
     if layer == "mpnn2":                     # gcn.py:113-150
-        e = torch.cat([x[b, snd], x[b, rcv]], -1) @ t[pre + "mpnn2/msg/kernel"]
+        e = torch.cat([x[b, snd], x[b, rcv]], -1) @ t[pre + "mpnn2/msg_transform/kernel"]
         m = (seg_sum(e) / torch.clamp(cnt, min=1)[:, None]).reshape(B, n, H)
-        return torch.tanh(torch.cat([x, m], -1) @ t[pre + "mpnn2/node/kernel"])
+        return torch.tanh(torch.cat([x, m], -1) @ t[pre + "mpnn2/node_update/kernel"])
     # gat1: gcn.py:171-206, graph_ops.segment_softmax
-    z = x @ t[pre + "gat1/pre_att/kernel"]
-    att = torch.cat([z[b, snd], z[b, rcv]], -1) @ t[pre + "gat1/att/kernel"]
+    z = x @ t[pre + "gat1/pre_att_linear/kernel"]
+    att = torch.cat([z[b, snd], z[b, rcv]], -1) @ t[pre + "gat1/att_linear/kernel"]
     att = torch.nn.functional.leaky_relu(att, 0.2)
     ex = torch.exp(att)
     att = ex / seg_sum(ex)[seg]

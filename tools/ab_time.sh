@@ -1,4 +1,4 @@
-# usage: bash tools/r03_time.sh tag1 tag2 ...  : us/step of libddrl_hip_abl_<tag>.so at 4096 envs, 2 rounds
+# usage: bash tools/ab_time.sh tag1 tag2 ...  : us/step of libddrl_hip_abl_<tag>.so at 4096 envs, 2 rounds
 mkdir -p gpurun_out/ab
 for i in 1 2; do
   for v in "$@"; do
