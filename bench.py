@@ -518,8 +518,9 @@ def main():
         kernel = (f"k_update_ffn<{A}, {ks1}> grad + {coll} all-reduce + k_apply_adam per step" if ddp else
                   "k_update_ffn (fused PPO minibatch SGD, one launch per iteration)")
         # the fused launch keeps 2 workgroups (policy / value branch) per policy, one per CU,
-        # times the row split (DDRL_UPDATE_SPLIT, default 2; the data-parallel grad launch is unsplit)
-        split = 1 if ddp else (1 if os.environ.get("DDRL_UPDATE_SPLIT", "2") == "1" else 2)
+        # times the row split (DDRL_UPDATE_SPLIT, default 2); the data-parallel gradient launch
+        # splits the same way when its rows fill both halves (capi.cpp grad_split: > 64 rows)
+        split = 1 if os.environ.get("DDRL_UPDATE_SPLIT", "2") == "1" or (ddp and rows_per_step <= 64) else 2
         active_cus = 2 * P * split
         model = f"{P} {'shared' if P == 1 else 'independent'} fcnet 2x64 polic{'y' if P == 1 else 'ies'} (d={d}, A={A})"
     # algorithmic HBM bytes: each minibatch row's record fields read once per branch

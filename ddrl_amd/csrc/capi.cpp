@@ -257,7 +257,12 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
     c->gnn.part_stride = (np + 3) & ~3;   // 16-byte aligned tile rows (float4 partial stores)
     c->gnn.grad = c->pol[0].grad;
     rc = dalloc(c, &c->gnn.part, (size_t)(DDRL_MB / 4) * c->gnn.part_stride) || dalloc(c, &c->gnn.statp, 2 * (DDRL_MB / 4) * 8) ||
-         dalloc(c, &c->gnn.normp, (np + 255) / 256) || dalloc(c, &c->gnn.bp_cur, 2);
+         dalloc(c, &c->gnn.normp, (np + 255) / 256) || dalloc(c, &c->gnn.bp_cur, 2) || dalloc(c, &c->gnn.flags, 256) ||
+         dalloc(c, &c->gnn.gran, 256);
+    c->gnn.seq = 0;
+    c->gnn.err = c->err;
+    c->gnn.tail = 1;
+    if (const char* e = std::getenv("DDRL_GNN_TAIL")) c->gnn.tail = std::atoi(e) != 0;
     // the record chunk of the fused update is allocated by the first ddrl_ppo_update (forward-only
     // and data-parallel contexts never need it), sized to the schedule when that is shorter
     c->gnn.chunk = nullptr;

@@ -127,11 +127,71 @@ __device__ __forceinline__ float quad_next(float v) { return dpp_mov<0x39>(v); }
 // Nontemporal stores stream them out of the XCD's L2 while the kernel runs instead of
 // leaving 3.6 MB of dirty lines for the end-of-kernel write-back (C5: 20.9 -> 20.2 us per step;
 // the same for the reduction's and Adam's outputs measured no gain).
-__device__ __forceinline__ void pst(float* p, float v) { __builtin_nontemporal_store(v, p); }
-__device__ __forceinline__ void pst4(float* p, floatx4 v) {
-  __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(p));
+// The one-launch step (coh: the partials are read by other workgroups of the same launch, on
+// any XCD) stores them as relaxed device-scope atomics instead (sc1: written through to the
+// device's coherence point; gnn_tail).
+__device__ __forceinline__ void pst(bool coh, float* p, float v) {
+  if (coh) __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else __builtin_nontemporal_store(v, p);
+}
+__device__ __forceinline__ void pst4(bool coh, float* p, floatx4 v) {
+  if (coh) {
+    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+    __hip_atomic_store(q, ((unsigned long long)__float_as_uint(v[1]) << 32) | __float_as_uint(v[0]), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, ((unsigned long long)__float_as_uint(v[3]) << 32) | __float_as_uint(v[2]), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(p));
+  }
+}
+__device__ __forceinline__ float cld(bool coh, const float* p) {
+  return coh ? __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+             : *p;
+}
+__device__ __forceinline__ void cst(bool coh, float* p, float v) {
+  if (coh) __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
 }
 __device__ __forceinline__ float leaky02(float x) { return x > 0.f ? x : 0.2f * x; }   // tf.nn.leaky_relu
+
+// Diagnostic build only (-DDDRL_GNN_STAMPS, tools/diag_gnn_stamps.py): s_memrealtime (100 MHz,
+// one clock for the whole chip) at the phase boundaries of the gradient launch, thread 0 of the
+// workgroups of tile 0 (both nets, every backward share), and at the start / end of block 0 of
+// the reduction and Adam launches; one row per step (plain stores); no stamp executes in the
+// real build.
+#ifdef DDRL_GNN_STAMPS
+#define GST_STEPS 4096
+#define GST_K 12
+__device__ unsigned long long g_gstamps[GST_STEPS][9][GST_K];   // [step][8 gradient WGs + reduce/adam][k]
+// start / end of EVERY workgroup of the three launches: [step][launch][block][start, end]
+#define GST_NB 256
+__device__ unsigned long long g_gspan[GST_STEPS][3][GST_NB][2];
+extern "C" int ddrl_diag_gnn_stamps(unsigned long long* host, unsigned long long* span) {
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gstamps), sizeof(g_gstamps)) != hipSuccess) return -1;
+  return span && hipMemcpyFromSymbol(span, HIP_SYMBOL(g_gspan), sizeof(g_gspan)) != hipSuccess ? -1 : 0;
+}
+#define SPAN(launch, blk, k)                                                                        \
+  do {                                                                                              \
+    if (threadIdx.x == 0 && ga.step < GST_STEPS && (blk) < GST_NB)                                  \
+      g_gspan[ga.step][launch][blk][k] = __builtin_amdgcn_s_memrealtime();                          \
+  } while (0)
+#define RSTAMPB(b, k)                                                                               \
+  do {                                                                                              \
+    if (threadIdx.x == 0 && (b) == 0 && ga.step < GST_STEPS)                                        \
+      g_gstamps[ga.step][8][k] = __builtin_amdgcn_s_memrealtime();                                  \
+  } while (0)
+#define GSTAMP(k)                                                                                   \
+  do {                                                                                              \
+    if (MODE == GNN_GRAD && threadIdx.x == 0 && blockIdx.x == 0 && ga.step < GST_STEPS)            \
+      g_gstamps[ga.step][blockIdx.y * 4 + (blockIdx.z & 3)][k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define GSTAMP(k)
+#define RSTAMPB(b, k)
+#define SPAN(launch, blk, k)
+#endif
 
 template <int A, int MODE, int NET, int L>
 __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
@@ -143,6 +203,7 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
   const bool gvalid = graph < ga.n_graphs;
   const GnnNetOff off = gnn_net_off(A, NET, L);
   const float* __restrict__ th = ga.theta;
+  GSTAMP(0);
   if (MODE == GNN_ACT && NET == 0 && ga.bootstrap) return;   // bootstrap: critic only
 #ifdef DDRL_ABL_GNN_EMPTY
   if (MODE == GNN_GRAD) return;
@@ -220,6 +281,10 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
 #pragma unroll
     for (int o = 0; o < O; ++o) wo[r][o] = th[off.wout + (16 * w + 4 * q + r) * O + o];
 
+#ifdef DDRL_GNN_STAMPS
+  wait_vmcnt0();   // diagnostic build: the weight / record loads have landed
+  GSTAMP(10);
+#endif
   // ---- hypernetwork + per-node encoding (partial over this wave's feature rows) ----
   floatx4 hacc[4];
 #pragma unroll
@@ -242,6 +307,7 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) part[w * 1024 + (4 * t + r) * 64 + lane] = hacc[t][r];
   __syncthreads();
+  GSTAMP(1);
   float* himg = lds + L_H;
   {
     // wave w finalizes feature block t = w: h = tanh(sum of the four partials, fixed order)
@@ -258,6 +324,7 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
   for (int fb = 0; fb < 4; ++fb)
 #pragma unroll
     for (int r = 0; r < 4; ++r) h[fb][r] = himg[wbase(r) + 16 * fb];
+  GSTAMP(2);
 
   // ---- message-passing layer: output block w of y (lane: node c, features 16 w + 4 q + r) ----
   float y[4];
@@ -332,6 +399,7 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
     for (int r = 0; r < 4; ++r)
       y[r] = tanh_fast(aSp * quad_prev(zf[r]) + aSs * zf[r] + aSn * quad_next(zf[r]));
   }
+  GSTAMP(3);
   // ---- head: partial dot over this wave's 16 features, then across waves ----
   float* hp = lds + L_HP;
 #pragma unroll
@@ -409,6 +477,7 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
   // ===================== GNN_GRAD: loss + backward + partial gradients ==================
   const UpdateArgs& U = ga.u;
   const UpdateHyper& H = ga.h;
+  const bool coh = ga.tail;    // one-launch step: partials read by this launch's reducers
   float* dsh = lds + L_DOUT;   // [4 graphs][4]
   float* sts = lds + L_ST;     // [4 graphs][8]
   if (tid < 16) {
@@ -442,12 +511,13 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
     }
   }
   __syncthreads();
+  GSTAMP(4);
   // per-tile statistics partial (fixed order over the 4 graphs)
   const int zs = (int)blockIdx.z;   // backward share of this workgroup (0 .. GNN_Z - 1)
   if (tid < 5 && zs == 0) {
     float s = 0.f;
     for (int gg = 0; gg < 4; ++gg) s += (4 * tile + gg < ga.n_graphs) ? sts[gg * 8 + tid] : 0.f;
-    ga.statp[(NET * (DDRL_MB / 4) + tile) * 8 + tid] = s;
+    cst(coh, ga.statp + (NET * (DDRL_MB / 4) + tile) * 8 + tid, s);
   }
   float* P = ga.part + (size_t)tile * ga.part_stride;
   const bool is_sel = n == sel;
@@ -463,18 +533,18 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
 #pragma unroll
       for (int o = 0; o < 4; ++o) v[4 * r + o] = y[r] * ds[o];
     const float s = row16_transpose_sum(v);
-    pst(P + off.wout + (16 * w + 4 * q + (c >> 2)) * 4 + (c & 3), s);
+    pst(coh, P + off.wout + (16 * w + 4 * q + (c >> 2)) * 4 + (c & 3), s);
   } else {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float v = row16_sum(y[r] * ds[0]);
-      if (c == 0) pst(P + off.wout + (16 * w + 4 * q + r) * O, v);
+      if (c == 0) pst(coh, P + off.wout + (16 * w + 4 * q + r) * O, v);
     }
   }
   if (tid < O && zs == 0) {
     float s = 0.f;
     for (int gg = 0; gg < 4; ++gg) s += dsh[gg * 4 + tid] * (4 * tile + gg < ga.n_graphs ? 1.f : 0.f);
-    pst(P + off.bout + tid, s);
+    pst(coh, P + off.bout + tid, s);
   }
   // dy -> du = dy (1 - y^2): gradient at the layer's pre-activation (lane: node c, block w)
   float du[4];
@@ -601,8 +671,8 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
         const float a1 = row16_sum(dps * zf[r]);
         const float a2 = row16_sum(dur * zf[r]);
         if (c == 0) {
-          pst(P + off.wnode + 16 * w + 4 * q + r, a1);
-          pst(P + off.wnode + 64 + 16 * w + 4 * q + r, a2);
+          pst(coh, P + off.wnode + 16 * w + 4 * q + r, a1);
+          pst(coh, P + off.wnode + 64 + 16 * w + 4 * q + r, a2);
         }
       }
     }
@@ -614,6 +684,7 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
     acc_t(dh, wpb, dmimg);   // dh = Wp . dz^T
     tA[0] = himg; tB[0] = dmimg; tP[0] = off.wmsg;
   }
+  GSTAMP(5);
   // the hypernet partials are consumed: reuse PART for the dz exchange [block][r][lane]
 #pragma unroll
   for (int r = 0; r < 4; ++r) part[(4 * w + r) * 64 + lane] = dh[r] * (1.f - h[w][r] * h[w][r]);
@@ -628,9 +699,11 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
     const floatx4 t = dw_tile<16>(tA[mat], tB[mat], kb, ob);
     const int base = tP[mat] + 16 * ob + c;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) pst(P + base + (16 * kb + 4 * q + r) * 64, t[r]);
+    for (int r = 0; r < 4; ++r) pst(coh, P + base + (16 * kb + 4 * q + r) * 64, t[r]);
   }
+  GSTAMP(6);
   __syncthreads();
+  GSTAMP(7);
   float dz[4][4];
 #pragma unroll
   for (int t = 0; t < 4; ++t)
@@ -652,6 +725,7 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
   float qb[4];
 #pragma unroll
   for (int s4 = 0; s4 < 4; ++s4) qb[s4] = c < 4 ? qt[(4 * s4 + q) * 4 + c] : (c == 4 ? 1.f : 0.f);
+  GSTAMP(8);
   // Software-pipelined over the feature rows i of this wave: the dpre tiles of row k + 1 are
   // computed (MFMA, tanh: VALU) and stored to the other half of a double-buffered LDS tile
   // while the 16 weight-gradient MFMAs of row k run on operands already in registers.
@@ -699,10 +773,11 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) acc = mfma4(tpb[256 * t + (4 * s4 + q) * 16 + c], qb[s4], acc);
         const int j = i * 64 + 16 * t + 4 * q;
-        if (c < 4) pst4(P + off.wenc + c * GHE + j, acc);
-        else if (c == 4) pst4(P + off.benc + j, acc);
+        if (c < 4) pst4(coh, P + off.wenc + c * GHE + j, acc);
+        else if (c == 4) pst4(coh, P + off.benc + j, acc);
       }
     }
+    GSTAMP(9);
     return;
   }
   dpre_tiles(0, tpb);
@@ -727,17 +802,25 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
       const int j = i * 64 + 16 * t + 4 * q;                  // acc[r]: column j + r, qd = c
-      if (c < 4) pst4(P + off.wenc + c * GHE + j, acc[t]);
-      else if (c == 4) pst4(P + off.benc + j, acc[t]);
+      if (c < 4) pst4(coh, P + off.wenc + c * GHE + j, acc[t]);
+      else if (c == 4) pst4(coh, P + off.benc + j, acc[t]);
     }
   }
 }
 
+__device__ __forceinline__ void gnn_tail(const GnnArgs& ga, int* bsh);   // below: the one-launch step
+
 template <int A, int MODE, int L>
 __global__ void __launch_bounds__(256) k_gnn(GnnArgs ga) {
   __shared__ float lds[L_TOTAL];
+  const int blk = blockIdx.x + gridDim.x * (blockIdx.y + 2 * blockIdx.z);
+  if (MODE == GNN_GRAD) SPAN(0, blk, 0);
   if (blockIdx.y == 0) gnn_tile<A, MODE, 0, L>(ga, lds);
   else gnn_tile<A, MODE, 1, L>(ga, lds);
+  if (MODE == GNN_GRAD) SPAN(0, blk, 1);
+  (void)blk;
+  if constexpr (MODE == GNN_GRAD)
+    if (ga.tail) gnn_tail(ga, reinterpret_cast<int*>(lds));
 }
 // k_gnn instance of a layer (MODE fixed)
 #define GNN_LAUNCH(MODE, L_, grid, s, ga)                                                            \
@@ -753,12 +836,12 @@ __global__ void __launch_bounds__(256) k_gnn(GnnArgs ga) {
 // ---- reduction over tiles: grad[p] = sum_t part[t][p] (fixed order) + norm^2 partials ----
 // loss statistics of the step: statp [net][tile][8]; lane j < 10 sums (net, stat) j over the
 // tiles (independent loads), lane 0 combines
-__device__ __forceinline__ void gnn_step_stats(const GnnArgs& ga, int ntiles) {
+__device__ __forceinline__ void gnn_step_stats(const GnnArgs& ga, int ntiles, bool coh = false) {
   __shared__ float sv[10];
   const int j = threadIdx.x, b = j / 5, k = j - 5 * b;
   float sv_t[DDRL_MB / 4];
 #pragma unroll
-  for (int t = 0; t < DDRL_MB / 4; ++t) sv_t[t] = t < ntiles ? ga.statp[(b * DDRL_MB / 4 + t) * 8 + k] : 0.f;
+  for (int t = 0; t < DDRL_MB / 4; ++t) sv_t[t] = t < ntiles ? cld(coh, ga.statp + (b * DDRL_MB / 4 + t) * 8 + k) : 0.f;
   float a = 0.f;
 #pragma unroll
   for (int t = 0; t < DDRL_MB / 4; ++t) a += sv_t[t];
@@ -781,53 +864,90 @@ __device__ __forceinline__ void gnn_step_stats(const GnnArgs& ga, int ntiles) {
   }
 }
 
-// The last block of the grid (one past the parameter blocks) sums the step's loss statistics
-// instead, in parallel with the parameter blocks (not after block 0's parameters).
-__global__ void __launch_bounds__(256) k_gnn_reduce(GnnArgs ga, int ntiles, int n) {
-  __shared__ float red[4];
-  if (blockIdx.x == gridDim.x - 1) {
-    if (threadIdx.x < 10) gnn_step_stats(ga, ntiles);
-    return;
+// Bounded waits of the one-launch step (gnn_tail below): an arrival flag / a tagged granule.
+__device__ __forceinline__ bool gnn_wait_tag(const GnnArgs& ga, const unsigned* flag, unsigned long long t0) {
+  for (;;) {
+    if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ga.tag) return true;
+    const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
+    if (dt > 20000ull && __hip_atomic_load(ga.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+    if (dt > 300000000ull) {   // 3 s
+      __hip_atomic_store(ga.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
   }
-  const int p = blockIdx.x * 256 + threadIdx.x;
+}
+__device__ __forceinline__ float gnn_wait_gran(const GnnArgs& ga, const unsigned long long* g, unsigned long long t0,
+                                               bool& ok) {
+  for (;;) {
+    const unsigned long long v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((unsigned)(v >> 32) == ga.tag) return __uint_as_float((unsigned)v);
+    const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
+    if ((dt > 20000ull && __hip_atomic_load(ga.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) || dt > 300000000ull) {
+      __hip_atomic_store(ga.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ok = false;
+      return 0.f;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// ---- reduction over tiles: grad[p] = sum_t part[t][p] (fixed order) + norm^2 partials ----
+// Reduction block b (256 parameters): this thread's summed gradient (parameter b * 256 + tid) is
+// returned; the block's squared-norm partial goes to normp[b] (coh: the tagged granule gran[b]).
+__device__ __forceinline__ float gnn_reduce_block(const GnnArgs& ga, int b, int ntiles, int n, bool store_grad,
+                                                  bool coh = false) {
+  __shared__ float red[4];
+  const int p = b * 256 + threadIdx.x;
   // all tile partials of this parameter in flight at once (a runtime-bound loop would wait
   // for each load before the next add), then summed in tile order
   float v[DDRL_MB / 4];
 #pragma unroll
   for (int t = 0; t < DDRL_MB / 4; ++t)
-    v[t] = (p < n && t < ntiles) ? ga.part[(size_t)t * ga.part_stride + p] : 0.f;
+    v[t] = (p < n && t < ntiles) ? cld(coh, ga.part + (size_t)t * ga.part_stride + p) : 0.f;
   float s = 0.f;
 #pragma unroll
   for (int t = 0; t < DDRL_MB / 4; ++t) s += v[t];
-  if (p < n) ga.grad[p] = s;
+  if (store_grad && p < n) ga.grad[p] = s;
   float ss = wave_sum(s * s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
   __syncthreads();
-  if (threadIdx.x == 0) ga.normp[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+  if (threadIdx.x == 0) {
+    const float np = ((red[0] + red[1]) + red[2]) + red[3];
+    if (coh)
+      __hip_atomic_store(ga.gran + b, ((unsigned long long)ga.tag << 32) | __float_as_uint(np), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    else
+      ga.normp[b] = np;
+  }
+  return p < n ? s : 0.f;
 }
 
-// ---- tf.clip_by_global_norm + tf1 Adam over all parameters of the policy ----
-__global__ void __launch_bounds__(256) k_gnn_adam(GnnArgs ga, int nred, int n) {
+// ---- tf.clip_by_global_norm + tf1 Adam on the 256 parameters of block b ----
+// g0, mi, vi, th0: this thread's gradient and state (loaded by the caller, ahead of the norm it
+// waits on); b1p, b2p: the step's beta powers.  coh: the norm^2 partials are the tagged
+// granules of this launch's reduction blocks (waited for, bounded; false = abandoned).
+__device__ __forceinline__ bool gnn_adam_block(const GnnArgs& ga, int b, int nred, int n, float g0, float mi,
+                                               float vi, float th0, float b1p, float b2p, bool coh = false) {
   __shared__ float scale_s;
+  __shared__ int ok_s;
   const UpdateArgs& U = ga.u;
   const UpdateHyper& h = ga.h;
-  // this thread's parameter state first: its loads do not depend on the clip scale and
-  // overlap the squared-norm reduction below
-  const int p = blockIdx.x * 256 + threadIdx.x;
+  const int p = b * 256 + threadIdx.x;
   const bool pv = p < n;
-  const float g0 = pv ? ga.grad[p] : 0.f;
-  float mi = pv ? U.m[p] : 0.f, vi = pv ? U.v[p] : 0.f;
-  const float th0 = pv ? U.theta[p] : 0.f;
-  const float b1p = ga.bp_cur[0], b2p = ga.bp_cur[1];
   if (threadIdx.x < 64) {
     // squared-norm partials of the reduction blocks: the same butterfly in every block
     float part = 0.f;
-    for (int b = threadIdx.x; b < nred; b += 64) part += ga.normp[b];
+    bool ok = true;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (int k = threadIdx.x; k < nred; k += 64) part += coh ? gnn_wait_gran(ga, ga.gran + k, t0, ok) : ga.normp[k];
     const float tot = wave_sum(part);
+    ok = __all(ok);
     if (threadIdx.x != 0) goto done;
+    ok_s = ok;
     const float gn = sqrtf(tot);
     scale_s = h.grad_clip * fminf(1.f / gn, 1.f / h.grad_clip);
-    if (blockIdx.x == 0) {
+    if (b == 0 && ok) {
       if (U.stats) {
         U.stats[(size_t)ga.step * 8 + 6] = gn;
         U.stats[(size_t)ga.step * 8 + 7] = scale_s;
@@ -838,7 +958,8 @@ __global__ void __launch_bounds__(256) k_gnn_adam(GnnArgs ga, int nred, int n) {
   }
 done:
   __syncthreads();
-  if (!pv) return;
+  if (!ok_s) return false;
+  if (!pv) return true;
   const float alpha = h.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   const float g = g0 * scale_s;
   mi = mi + (g - mi) * (1.f - h.b1);
@@ -846,6 +967,104 @@ done:
   U.m[p] = mi;
   U.v[p] = vi;
   U.theta[p] = th0 - (mi * alpha) / (sqrtf(vi) + h.eps);
+  return true;
+}
+
+// Three-launch step: the last block of the reduction grid (one past the parameter blocks) sums
+// the step's loss statistics instead, in parallel with the parameter blocks.
+__global__ void __launch_bounds__(256) k_gnn_reduce(GnnArgs ga, int ntiles, int n) {
+  RSTAMPB(blockIdx.x, 0);
+  SPAN(1, blockIdx.x, 0);
+  if (blockIdx.x == gridDim.x - 1) {
+    if (threadIdx.x < 10) gnn_step_stats(ga, ntiles);
+    SPAN(1, blockIdx.x, 1);
+    return;
+  }
+  (void)gnn_reduce_block(ga, blockIdx.x, ntiles, n, true);
+  RSTAMPB(blockIdx.x, 1);
+  SPAN(1, blockIdx.x, 1);
+}
+
+__global__ void __launch_bounds__(256) k_gnn_adam(GnnArgs ga, int nred, int n) {
+  RSTAMPB(blockIdx.x, 2);
+  SPAN(2, blockIdx.x, 0);
+  const UpdateArgs& U = ga.u;
+  // this thread's parameter state first: its loads do not depend on the clip scale and
+  // overlap the squared-norm reduction
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  const bool pv = p < n;
+  const float g0 = pv ? ga.grad[p] : 0.f;
+  const float mi = pv ? U.m[p] : 0.f, vi = pv ? U.v[p] : 0.f;
+  const float th0 = pv ? U.theta[p] : 0.f;
+  (void)gnn_adam_block(ga, blockIdx.x, nred, n, g0, mi, vi, th0, ga.bp_cur[0], ga.bp_cur[1]);
+  RSTAMPB(blockIdx.x, 3);
+  SPAN(2, blockIdx.x, 1);
+}
+
+// ---- one-launch step: the reduction and Adam run in the gradient launch's tail ----
+// The reduction needs every tile's partials and Adam the global norm, so the step used to be
+// three launches (two kernel boundaries of ~1.5-2 us each, MI355X_MICROARCH.md "boundary").
+// Here the first nred + 1 workgroups of the gradient grid (linear block id b) are also the
+// reduction blocks (b = nred sums the loss statistics).  Every workgroup, once its partials and
+// statistics are written, raises its arrival flag (flag[block] = this launch's tag); a
+// reduction block, after its own tile, waits until every flag carries the tag (one flag per
+// thread), runs the reduction block's code, publishes its norm^2 partial as a tagged granule
+// {value, tag}, waits for the granules of all nred blocks (the same butterfly order as
+// k_gnn_adam) and runs the Adam block's code on its 256 parameters.  Same blocks, same order of
+// every sum as the three-launch step: bit-identical results (tests/test_gpu_gnn.py).
+// Protocol: every value another workgroup reads (partials, loss statistics, flags, granules) is
+// a relaxed device-scope atomic store (sc1: written through to the device's coherence point)
+// and load; a flag or granule is written only after an s_waitcnt on the stores it covers.  No
+// read-modify-write counter: 256 arrivals on one device-scope atomic serialize at ~12 ns each
+// (MI355X_MICROARCH.md "fanin"), measured 22.7 us per step against 18.9 for three launches, and
+// release / acquire orderings (an L2 write-back per arrival, an L2 invalidate per poll) 33.1.
+// The waiting workgroups wait only on workgroups of the same grid, at most one per CU, so all
+// are resident; every wait is bounded (the error word, as the fcnet exchanges; the host
+// restores its snapshot).
+__device__ __forceinline__ void gnn_tail(const GnnArgs& ga, int* bsh) {
+  const int ngrid = (int)(gridDim.x * gridDim.y * gridDim.z);
+  const int b = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
+  // every wave's partial and statistics stores have completed before the flag goes up
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(ga.flags + b, ga.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (b > ga.nred) return;
+  // a reduction block: every workgroup of the grid has arrived (one flag per thread)
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  const bool ok = (int)threadIdx.x >= ngrid || gnn_wait_tag(ga, ga.flags + threadIdx.x, t0);
+  if (!__syncthreads_and(ok)) return;
+  RSTAMPB(b, 0);
+  SPAN(1, b, 0);
+  if (b == ga.nred) {   // the loss statistics of the step
+    if (threadIdx.x < 10) gnn_step_stats(ga, ga.ntiles, true);
+    SPAN(1, b, 1);
+    return;
+  }
+  const UpdateArgs& U = ga.u;
+  const int n = ga.n_params;
+  // the parameter state first (its loads overlap the partials'), and the beta powers: read by
+  // thread 0 and landed before this block's granule goes up below (block 0 writes the next beta
+  // powers only once every granule is there)
+  const int p = b * 256 + threadIdx.x;
+  const bool pv = p < n && !U.grad_out;
+  const float mi = pv ? U.m[p] : 0.f, vi = pv ? U.v[p] : 0.f;
+  const float th0 = pv ? U.theta[p] : 0.f;
+  float* bps = reinterpret_cast<float*>(bsh);
+  if (threadIdx.x == 0 && !U.grad_out) {
+    bps[0] = U.beta_pow[0];
+    bps[1] = U.beta_pow[1];
+    __builtin_amdgcn_s_waitcnt(0);
+  }
+  const float g0 = gnn_reduce_block(ga, b, ga.ntiles, n, U.grad_out != nullptr, true);   // syncs
+  RSTAMPB(b, 1);
+  SPAN(1, b, 1);
+  if (U.grad_out) return;   // data-parallel gradient: the all-reduce and Adam follow as launches
+  const float b1p = bps[0], b2p = bps[1];
+  RSTAMPB(b, 2);
+  SPAN(2, b, 0);
+  (void)gnn_adam_block(ga, b, ga.nred, n, g0, mi, vi, th0, b1p, b2p, true);
+  RSTAMPB(b, 3);
+  SPAN(2, b, 1);
 }
 
 // Pre-gather of a run of minibatch steps: dst[k][i][col] = rec[shuffle[perm[e][b] * 128 + i]][col]
@@ -901,7 +1120,7 @@ void launch_forward_gnn(hipStream_t s, const ForwardArgs& fa, int layer) {
 }
 
 void launch_step_gnn(hipStream_t s, const UpdateArgs& u, const UpdateHyper& h, int step, int nrows, float inv_n,
-                     const GnnScratch& sc, const float* stage, int layer) {
+                     GnnScratch& sc, const float* stage, int layer) {
   check_a(u.A);
   GnnArgs ga{};
   ga.theta = u.theta; ga.u = u; ga.h = h; ga.step = step; ga.n_graphs = nrows; ga.inv_n = inv_n;
@@ -910,12 +1129,22 @@ void launch_step_gnn(hipStream_t s, const UpdateArgs& u, const UpdateHyper& h, i
   ga.stage = stage;
   const int ntiles = (nrows + 3) / 4;
   const int n = gnn_param_total(u.A, layer);
+  const int nred = (n + 255) / 256;
+  const int ngrid = ntiles * 2 * GNN_Z;
+  ga.ntiles = ntiles; ga.n_params = n; ga.nred = nred; ga.err = sc.err; ga.flags = sc.flags; ga.gran = sc.gran;
+  // one launch per step when the gradient grid can host the nred + 1 reduction blocks (and every
+  // workgroup one flag per reduction-block thread)
+  ga.tail = sc.tail && sc.flags && ngrid >= nred + 1 && ngrid <= 256;
+  if (ga.tail) {
+    if (++sc.seq == 0) sc.seq = 1;   // tags never 0 (the buffers start zeroed)
+    ga.tag = sc.seq;
+  }
   // tiles of the critic write their statistics after the actor's: statp [2][32][8]
   GNN_LAUNCH(GNN_GRAD, layer, dim3(ntiles, 2, GNN_Z), s, ga);
-  const int nred = (n + 255) / 256;
 #ifdef DDRL_ABL_GNN_GRAD_ONLY   // ablation build (timing only): no reduction / Adam launches
   return;
 #endif
+  if (ga.tail) return;
   hipLaunchKernelGGL(k_gnn_reduce, dim3(nred + 1), dim3(256), 0, s, ga, ntiles, n);
   if (!u.grad_out) hipLaunchKernelGGL(k_gnn_adam, dim3(nred), dim3(256), 0, s, ga, nred, n);
 }

@@ -189,18 +189,25 @@ struct GnnArgs {
   // staged minibatch (fused update only): the records of this step, contiguous [128][stride]
   // (a slot of the pre-gathered chunk); null: gather through shuffle / perm
   const float* stage;
+  // one-launch step (gnn.hip gnn_tail): arrival flags [256], norm^2 granules [256], this launch's tag
+  unsigned* flags; unsigned long long* gran; unsigned tag; int tail; int nred; int n_params; int ntiles; int* err;
 };
 struct GnnScratch {
   float* part; int part_stride; float* statp; float* normp; float* bp_cur; float* grad;
   float* chunk;       // [chunk_steps][128][stride] records of a run of minibatch steps
   int chunk_steps;    // min(GNN_CHUNK_STEPS, the schedule's steps); chunk allocated on first use
+  unsigned* flags;              // [256] arrival flags of the one-launch step (device)
+  unsigned long long* gran;     // [256] tagged norm^2 partials {value, tag} of its reduction blocks
+  unsigned seq;                 // tag of the last one-launch step (host; never 0)
+  int tail;           // 1: reduction + clip + Adam in the gradient launch (DDRL_GNN_TAIL, default 1)
+  int* err;           // the context's error word
 };
 #define GNN_CHUNK_STEPS 1024
 int gnn_param_total(int A, int layer);   // layer: DDRL_GNN_*
 // stage: the step's pre-gathered records (fused update) or null (data-parallel gradient of
 // explicit rows)
 void launch_step_gnn(hipStream_t s, const UpdateArgs& u, const UpdateHyper& h, int step, int nrows, float inv_n,
-                     const GnnScratch& sc, const float* stage, int layer);
+                     GnnScratch& sc, const float* stage, int layer);
 // the records of minibatch steps [step0, step0 + n_steps) of the schedule -> dst
 // ([n_steps][128][stride], n_steps <= GNN_CHUNK_STEPS): one bandwidth-bound gather per chunk
 void launch_gnn_gather(hipStream_t s, const UpdateArgs& u, int step0, int n_steps, float* dst);

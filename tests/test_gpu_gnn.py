@@ -222,3 +222,51 @@ def test_gnn_update_across_record_chunks():
                s0["grad_gnorm"]]
         _close(st[k, :7], np.array(ref, np.float32), rtol=1e-4, atol=1e-5, msg=f"stats step {k}")
     ctx.close()
+
+
+def test_gnn_one_launch_step_equals_three_launch_step(monkeypatch):
+    """Round 4: the GNN training step in ONE launch (the reduction and clip + Adam run in the
+    gradient launch's tail, by its last-arriving workgroups; gnn.hip gnn_tail) is bit-identical to
+    the three-launch step (DDRL_GNN_TAIL=0: k_gnn -> k_gnn_reduce -> k_gnn_adam) over the whole
+    100-step schedule: parameters, Adam m / v, beta powers and every step's learner statistics.
+    Also the data-parallel gradient (ddrl_ppo_grad of 128 rows: reduction in the tail, Adam left
+    to the caller) against the three-launch gradient."""
+    import torch
+    from ddrl_amd import native as N
+    layer = "mpnn"   # the tail runs after the layer code, the same for every layer
+    ctx0, cfg, orc, norms, params, _, _ = _rollout(32, 10, 81, head_scale=1.0)
+    ctx0.close()
+    ctxs = []
+    for tail in ("1", "0"):
+        monkeypatch.setenv("DDRL_GNN_TAIL", tail)
+        c = N.Context(cfg, 0, torch.cuda.current_stream().cuda_stream)
+        lay = c.layout[0]
+        rec = orc.flat_records(0, lay)
+        c.records_set(0, rec)
+        c.adv_norm_set(0, *norms[0])
+        c.params_set(0, O.pack(params, O.gnn_param_shapes(4, layer=layer)))
+        ctxs.append(c)
+    monkeypatch.delenv("DDRL_GNN_TAIL")
+    sh, pe = O.sgd_schedule(np.random.default_rng(17), rec.shape[0], 128, cfg.num_sgd_iter)
+    steps = cfg.num_sgd_iter * (rec.shape[0] // 128)
+    rows = torch.from_numpy(sh[:128].copy()).cuda()
+    grads = []
+    for c in ctxs:
+        g = torch.zeros(c.n_params[0], device="cuda")
+        c.ppo_grad(0, rows, 128, 0.2, g)
+        c.synchronize()
+        grads.append(g.cpu().numpy())
+        c.ppo_update(1, [torch.from_numpy(sh).cuda()], [torch.from_numpy(pe).cuda()], [0.2])
+        c.synchronize()
+    np.testing.assert_array_equal(grads[0], grads[1])
+    a, b = ctxs
+    np.testing.assert_array_equal(a.params_get(0), b.params_get(0))
+    ma, va, b1a, b2a = a.adam_get(0)
+    mb, vb, b1b, b2b = b.adam_get(0)
+    np.testing.assert_array_equal(ma, mb)
+    np.testing.assert_array_equal(va, vb)
+    assert (b1a, b2a) == (b1b, b2b)
+    np.testing.assert_array_equal(a.ppo_stats(0, steps), b.ppo_stats(0, steps))
+    assert not np.array_equal(a.params_get(0), O.pack(params, O.gnn_param_shapes(4, layer=layer)))
+    for c in ctxs:
+        c.close()

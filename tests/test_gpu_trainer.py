@@ -400,8 +400,10 @@ def test_trainer_host_backend_runs_the_reference_curriculum_callback():
         result = info["result"]
         trainer = info["trainer"]
         timesteps_res = result["timesteps_total"]
-        seen.append(trainer.workers.foreach_worker(
-            lambda ev: ev.foreach_env(lambda env: env.update_environment_after_epoch(timesteps_res))))
+        before = trainer.backend.target_velocities
+        trainer.workers.foreach_worker(
+            lambda ev: ev.foreach_env(lambda env: env.update_environment_after_epoch(timesteps_res)))
+        seen.append((before, trainer.backend.target_velocities))
 
     tr = PPOTrainer({"env": "QuantrupedMultiEnv_Local", "rollout_fragment_length": 8, "env_backend": "host",
                      "env_config": {"target_velocity": [0.5, 1.5]},
@@ -411,7 +413,7 @@ def test_trainer_host_backend_runs_the_reference_curriculum_callback():
     assert tr.cfg.obs_full_dim == 44
     r = tr.train()
     assert len(seen) == 1 and r["timesteps_total"] == 8 * 64
-    np.testing.assert_array_equal(tr.backend.target_velocities, tv0)   # kept by the reset
+    np.testing.assert_array_equal(seen[0][1], seen[0][0])   # the reset keeps every env's velocity
     for pid, st in r["info"]["learner"].items():
         assert np.isfinite(st["total_loss"]), pid
     tr.train()

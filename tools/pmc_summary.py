@@ -1,44 +1,118 @@
-"""HBM traffic per minibatch step of the update kernels from the rocprofv3 PMC passes of
-tools/profile_r02.sh / profile_r03.sh (FETCH_SIZE and WRITE_SIZE in separate runs, kB per dispatch).
+"""Per-step HBM traffic, matrix-core busy fraction and effective clock of the update kernels from
+the rocprofv3 PMC passes of tools/profile_r04.sh (earlier rounds: profile_r02.sh / r03.sh, the
+traffic part only).
 
-    python tools/pmc_summary.py gpurun_out/prof > profiles/r02/pmc_summary.json
+    python tools/pmc_summary.py gpurun_out/prof4 > profiles/r04/pmc_summary.json
 
-FETCH_SIZE is doubled per MI355X_MICROARCH.md (gfx950 tallies 128-B requests at 64 B).
-Per workload the bytes of every update-kernel dispatch are summed and divided by the
-minibatch steps they cover:
+Traffic: FETCH_SIZE and WRITE_SIZE come from separate passes (kB per dispatch); FETCH_SIZE is
+doubled per MI355X_MICROARCH.md (gfx950 tallies 128-B requests at 64 B).  Per workload the
+bytes of every update-kernel dispatch are summed and divided by the minibatch steps they cover:
   local: one fused k_update_ffn launch = 10 epochs x 6400 steps x 4 policies (4096 envs)
   c4:    one fused launch = 10 x 25600 steps x 1 policy (SharedDecentral, 4096 envs)
   c5:    k_gnn<2, 2> + k_gnn_reduce + k_gnn_adam per step (+ k_gnn_gather per 1024 steps),
          10 x 800 steps (128 envs)
+
+Matrix cores and clock (pass "MFMA": SQ_VALU_MFMA_BUSY_CYCLES, SQ_BUSY_CYCLES, SQ_WAVE_CYCLES,
+GRBM_GUI_ACTIVE with --kernel-trace), per kernel summed over its dispatches:
+  * kernel cycles = GRBM_GUI_ACTIVE / 8 (rocprofv3 sums the counter over the 8 XCDs,
+    MI355X_MICROARCH.md "DVFS give-back");
+  * clock_ghz = kernel cycles / the dispatches' kernel-trace duration (the guide: within 3 % of
+    the in-kernel clock for dispatches of >= 10 ms, reads high below ~0.3 ms);
+  * SQ_VALU_MFMA_BUSY_CYCLES counts matrix-core busy cycles summed over the SIMDs
+    (= 32 per v_mfma_f32_16x16x4_f32, 2048 FLOP at 64 FLOP / cycle / SIMD);
+    mfma_busy_frac_chip = busy / (kernel cycles x 1024 SIMDs);
+    mfma_busy_frac_of_active_simds = busy / (kernel cycles x the SIMDs the launch occupies:
+    one wave per SIMD, 4 per workgroup, the workgroups that have work);
+  * mfma_flop_per_busy_cycle_per_simd = the kernel's algorithmic FLOP / busy: 64 when every
+    busy cycle does useful f32 work, lower when MFMAs run on zero padding.
 """
-import csv, json, os, sys
+import csv
+import json
+import os
+import sys
 
 GFX950_FETCH_CORRECTION = 2.0
+N_SIMD = 1024
 WORKLOADS = {
     "local": {"kernels": ["void k_update_ffn<2, 9"], "steps": 10 * 6400 * 4,
-              "workload": "QuantrupedMultiEnv_Local, 4096 envs, T=200 (one fused launch: 10 x 6400 steps x 4 policies)"},
+              "workload": "QuantrupedMultiEnv_Local, 4096 envs, T=200 (one fused launch: 10 x 6400 steps x 4 policies)",
+              # the dominant kernel, its occupied SIMDs (16 workgroups x 4 waves) and algorithmic
+              # FLOP per step (bench.py ffn_flops_per_row(35, 2) x 128 rows)
+              "mfma": {"kernel": "void k_update_ffn<2, 9", "active_simds": 64, "flop_per_step": 68992 * 128},
+              "also": ["void k_act_ffn<2, 9"]},
     "c4": {"kernels": ["void k_update_ffn<2, 5"], "steps": 10 * 25600,
-           "workload": "QuantrupedMultiEnv_SharedDecentral, 4096 envs, T=200 (one fused launch: 10 x 25600 steps)"},
+           "workload": "QuantrupedMultiEnv_SharedDecentral, 4096 envs, T=200 (one fused launch: 10 x 25600 steps)",
+           "mfma": {"kernel": "void k_update_ffn<2, 5", "active_simds": 16, "flop_per_step": 2 * (2 * (19 * 64 + 64 * 64 + 64 * 4 + 19 * 64 + 64 * 64 + 64) + (64 * 64 + 64 * 4) + (64 * 64 + 64)) * 128},
+           "also": ["void k_act_ffn<2, 5"]},
     "c5": {"kernels": ["void k_gnn<2, 2", "k_gnn_reduce", "k_gnn_adam", "k_gnn_gather"], "steps": 10 * 800,
            "workload": "QuantrupedMultiEnv_DecentralShared_Graph, 128 envs, T=200 (10 x 800 steps, 3 launches "
-                       "each, plus one record gather per 1024 steps)"},
+                       "each, plus one record gather per 1024 steps)",
+           "mfma": {"kernel": "void k_gnn<2, 2", "active_simds": 1024, "flop_per_step": None},
+           "also": ["void k_gnn<2, 0"]},
 }
+
+
+def _rows(path):
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            r["Kernel_Name"] = r["Kernel_Name"].replace("(anonymous namespace)::", "")
+            yield r
 
 
 def counter(path, name, prefix):
     tot, n = 0.0, 0
-    with open(path) as f:
-        for r in csv.DictReader(f):
-            kn = r["Kernel_Name"].replace("(anonymous namespace)::", "")   # r03: kernels in an unnamed namespace
-            if r["Counter_Name"] == name and kn.startswith(prefix):
-                tot += float(r["Counter_Value"])
-                n += 1
+    for r in _rows(path):
+        if r["Counter_Name"] == name and r["Kernel_Name"].startswith(prefix):
+            tot += float(r["Counter_Value"])
+            n += 1
     return tot, n
 
 
+def mfma_stats(d, prefix, active_simds, flop_per_dispatch=None):
+    """Matrix-core busy and clock of the dispatches of one kernel in pass directory d."""
+    cpath = os.path.join(d, "run_counter_collection.csv")
+    tpath = os.path.join(d, "run_kernel_trace.csv")
+    if not os.path.exists(cpath):
+        return None
+    per = {}
+    for r in _rows(cpath):
+        if not r["Kernel_Name"].startswith(prefix):
+            continue
+        k = r.get("Dispatch_Id") or r.get("Correlation_Id")
+        e = per.setdefault(k, {})
+        e[r["Counter_Name"]] = e.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        if r.get("Start_Timestamp") and r.get("End_Timestamp"):
+            e["ns"] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+    if not per:
+        return None
+    if os.path.exists(tpath) and any("ns" not in e for e in per.values()):
+        for r in _rows(tpath):
+            k = r.get("Dispatch_Id") or r.get("Correlation_Id")
+            if k in per:
+                per[k]["ns"] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+    tot = {}
+    for e in per.values():
+        for k, v in e.items():
+            tot[k] = tot.get(k, 0.0) + v
+    cyc = tot.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
+    busy = tot.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+    ns = tot.get("ns", 0.0)
+    out = {"kernel": prefix, "dispatches": len(per), "duration_ns": ns, "kernel_cycles": cyc,
+           "SQ_VALU_MFMA_BUSY_CYCLES": busy, "SQ_BUSY_CYCLES": tot.get("SQ_BUSY_CYCLES"),
+           "SQ_WAVE_CYCLES": tot.get("SQ_WAVE_CYCLES"), "GRBM_GUI_ACTIVE": tot.get("GRBM_GUI_ACTIVE"),
+           "clock_ghz": cyc / ns if ns > 0 else None,
+           "mfma_busy_frac_chip": busy / (cyc * N_SIMD) if cyc > 0 else None,
+           "active_simds": active_simds,
+           "mfma_busy_frac_of_active_simds": busy / (cyc * active_simds) if cyc > 0 and active_simds else None}
+    if flop_per_dispatch and busy > 0:
+        out["mfma_flop_per_busy_cycle_per_simd"] = flop_per_dispatch * len(per) / busy
+    return out
+
+
 def main(d):
-    out = {"command": "tools/profile_r0N.sh: rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE (separate passes) -- "
-                      "python3 bench.py --steps 1 --warmup 0 ...",
+    out = {"command": "tools/profile_r04.sh: rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | "
+                      "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE (separate passes, "
+                      "--kernel-trace) -- python3 bench.py --steps 1 --warmup 0 ...",
            "gfx950_fetch_correction": GFX950_FETCH_CORRECTION, "workloads": {}}
     for name, w in WORKLOADS.items():
         per = {}
@@ -52,11 +126,19 @@ def main(d):
             per[k] = {"dispatches": nf, "fetch_kb": f_kb, "write_kb": w_kb,
                       "hbm_bytes_per_step": round(b / w["steps"], 1)}
             total += b
-        out["workloads"][name] = {"workload": w["workload"], "steps": w["steps"], "kernels": per,
-                                  "hbm_bytes_per_step": round(total / w["steps"], 1)}
+        res = {"workload": w["workload"], "steps": w["steps"], "kernels": per,
+               "hbm_bytes_per_step": round(total / w["steps"], 1)}
+        m = w["mfma"]
+        mdir = os.path.join(d, f"pmc_{name}_MFMA")
+        flop = m["flop_per_step"] * w["steps"] if m["flop_per_step"] and name != "c5" else None
+        st = mfma_stats(mdir, m["kernel"], m["active_simds"], flop)
+        if st is not None:
+            res["mfma"] = st
+            res["mfma_other"] = [x for x in (mfma_stats(mdir, k, None) for k in w.get("also", [])) if x]
+        out["workloads"][name] = res
     json.dump(out, sys.stdout, indent=1)
     print()
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof")
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/prof4")
