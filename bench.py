@@ -509,7 +509,9 @@ def main():
     achieved_tf = flops_launch / (upd_avg_ms * 1e-3) / 1e12
     ks1 = (d + 3) // 4
     if gnn:
-        kernel = "k_gnn<GRAD> + k_gnn_reduce + k_gnn_adam (three launches per minibatch step)"
+        kernel = ("k_gnn<GRAD> + k_gnn_reduce + k_gnn_adam (three launches per minibatch step)"
+                  if os.environ.get("DDRL_GNN_TAIL", "1") == "0" or ddp else
+                  "k_gnn<GRAD> with the reduction and clip + Adam in its tail (one launch per minibatch step)")
         # (tiles of 4 graphs) x (actor, critic) x 4 backward shares (gnn.hip GNN_Z), one per CU
         active_cus = min(256, 2 * ((rows_per_step + 3) // 4) * 4)
         model = f"shared GraphNet/MPNN leg policy (4 nodes x 19 features + ego quaternion, A={A})"

@@ -258,8 +258,9 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
     c->gnn.grad = c->pol[0].grad;
     rc = dalloc(c, &c->gnn.part, (size_t)(DDRL_MB / 4) * c->gnn.part_stride) || dalloc(c, &c->gnn.statp, 2 * (DDRL_MB / 4) * 8) ||
          dalloc(c, &c->gnn.normp, (np + 255) / 256) || dalloc(c, &c->gnn.bp_cur, 2) || dalloc(c, &c->gnn.flags, 256) ||
-         dalloc(c, &c->gnn.gran, 256);
+         dalloc(c, &c->gnn.gran, 256) || dalloc(c, &c->gnn.plist, np);
     c->gnn.seq = 0;
+    c->gnn.lists = 0;
     c->gnn.err = c->err;
     c->gnn.tail = 1;
     if (const char* e = std::getenv("DDRL_GNN_TAIL")) c->gnn.tail = std::atoi(e) != 0;
@@ -351,6 +352,9 @@ static int check_err(ddrl_ctx* c) {
   HIPCHK(hipMemcpy(&e, c->err, sizeof(int), hipMemcpyDeviceToHost));
   if (e) {
     (void)hipMemset(c->err, 0, sizeof(int));
+    // a one-launch GNN step whose waits were abandoned (e.g. a broken XCD placement): the
+    // context goes on with the three-launch step
+    if (c->cfg.model_kind == DDRL_MODEL_GNN) c->gnn.tail = 0;
     const int bad = placement_broken(c);
     if (restore_snapshot(c)) return -1;
     c->snap_mask = 0;

@@ -39,6 +39,8 @@
 // fixed-order reduction over tiles + squared norm partials (k_gnn_reduce), and
 // clip_by_global_norm + tf1 Adam (k_gnn_adam).  A DDP step stops after the reduction.
 // (Reduction and Adam fused into one launch behind a grid barrier measured slower: DESIGN §3.)
+#include <vector>
+
 #include "common.h"
 #include "kernels.h"
 #include "ppo_loss.h"
@@ -127,32 +129,18 @@ __device__ __forceinline__ float quad_next(float v) { return dpp_mov<0x39>(v); }
 // Nontemporal stores stream them out of the XCD's L2 while the kernel runs instead of
 // leaving 3.6 MB of dirty lines for the end-of-kernel write-back (C5: 20.9 -> 20.2 us per step;
 // the same for the reduction's and Adam's outputs measured no gain).
-// The one-launch step (coh: the partials are read by other workgroups of the same launch, on
-// any XCD) stores them as relaxed device-scope atomics instead (sc1: written through to the
-// device's coherence point; gnn_tail).
-__device__ __forceinline__ void pst(bool coh, float* p, float v) {
-  if (coh) __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// The one-launch step (l2: the partials are read by reducers on the same XCD in the same
+// launch, gnn_tail) keeps them in the XCD's L2 with plain stores instead.
+#ifndef DDRL_GNN_L2_PLAIN
+#define DDRL_GNN_L2_PLAIN 0
+#endif
+__device__ __forceinline__ void pst(bool l2, float* p, float v) {
+  if (l2 && DDRL_GNN_L2_PLAIN) *p = v;
   else __builtin_nontemporal_store(v, p);
 }
-__device__ __forceinline__ void pst4(bool coh, float* p, floatx4 v) {
-  if (coh) {
-    unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
-    __hip_atomic_store(q, ((unsigned long long)__float_as_uint(v[1]) << 32) | __float_as_uint(v[0]), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(q + 1, ((unsigned long long)__float_as_uint(v[3]) << 32) | __float_as_uint(v[2]), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(p));
-  }
-}
-__device__ __forceinline__ float cld(bool coh, const float* p) {
-  return coh ? __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT))
-             : *p;
-}
-__device__ __forceinline__ void cst(bool coh, float* p, float v) {
-  if (coh) __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
+__device__ __forceinline__ void pst4(bool l2, float* p, floatx4 v) {
+  if (l2 && DDRL_GNN_L2_PLAIN) *reinterpret_cast<floatx4*>(p) = v;
+  else __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(p));
 }
 __device__ __forceinline__ float leaky02(float x) { return x > 0.f ? x : 0.2f * x; }   // tf.nn.leaky_relu
 
@@ -184,8 +172,8 @@ extern "C" int ddrl_diag_gnn_stamps(unsigned long long* host, unsigned long long
   } while (0)
 #define GSTAMP(k)                                                                                   \
   do {                                                                                              \
-    if (MODE == GNN_GRAD && threadIdx.x == 0 && blockIdx.x == 0 && ga.step < GST_STEPS)            \
-      g_gstamps[ga.step][blockIdx.y * 4 + (blockIdx.z & 3)][k] = __builtin_amdgcn_s_memrealtime(); \
+    if (MODE == GNN_GRAD && threadIdx.x == 0 && tile == 0 && ga.step < GST_STEPS)                   \
+      g_gstamps[ga.step][NET * 4 + (zs & 3)][k] = __builtin_amdgcn_s_memrealtime();                \
   } while (0)
 #else
 #define GSTAMP(k)
@@ -194,10 +182,9 @@ extern "C" int ddrl_diag_gnn_stamps(unsigned long long* host, unsigned long long
 #endif
 
 template <int A, int MODE, int NET, int L>
-__device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
+__device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds, const int tile, const int zs) {
   constexpr int O = NET ? 1 : 2 * A;
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, q = lane >> 4, w = tid >> 6;
-  const int tile = blockIdx.x;
   const int g = c >> 2, n = c & 3;
   const int graph = 4 * tile + g;
   const bool gvalid = graph < ga.n_graphs;
@@ -205,6 +192,7 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
   const float* __restrict__ th = ga.theta;
   GSTAMP(0);
   if (MODE == GNN_ACT && NET == 0 && ga.bootstrap) return;   // bootstrap: critic only
+  if (MODE == GNN_GRAD && ga.only_share >= 0 && zs != ga.only_share) return;   // owner discovery
 #ifdef DDRL_ABL_GNN_EMPTY
   if (MODE == GNN_GRAD) return;
 #endif
@@ -477,7 +465,7 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
   // ===================== GNN_GRAD: loss + backward + partial gradients ==================
   const UpdateArgs& U = ga.u;
   const UpdateHyper& H = ga.h;
-  const bool coh = ga.tail;    // one-launch step: partials read by this launch's reducers
+  const bool coh = ga.tail;    // one-launch step: partials read by this launch's reducers (pst)
   float* dsh = lds + L_DOUT;   // [4 graphs][4]
   float* sts = lds + L_ST;     // [4 graphs][8]
   if (tid < 16) {
@@ -512,12 +500,12 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
   }
   __syncthreads();
   GSTAMP(4);
-  // per-tile statistics partial (fixed order over the 4 graphs)
-  const int zs = (int)blockIdx.z;   // backward share of this workgroup (0 .. GNN_Z - 1)
+  // per-tile statistics partial (fixed order over the 4 graphs); zs: backward share of this
+  // workgroup (0 .. GNN_Z - 1)
   if (tid < 5 && zs == 0) {
     float s = 0.f;
     for (int gg = 0; gg < 4; ++gg) s += (4 * tile + gg < ga.n_graphs) ? sts[gg * 8 + tid] : 0.f;
-    cst(coh, ga.statp + (NET * (DDRL_MB / 4) + tile) * 8 + tid, s);
+    ga.statp[(NET * (DDRL_MB / 4) + tile) * 8 + tid] = s;
   }
   float* P = ga.part + (size_t)tile * ga.part_stride;
   const bool is_sel = n == sel;
@@ -808,19 +796,28 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds) {
   }
 }
 
-__device__ __forceinline__ void gnn_tail(const GnnArgs& ga, int* bsh);   // below: the one-launch step
+__device__ __forceinline__ void gnn_tail(const GnnArgs& ga, float* lds, int tile, int net, int zs);   // below
 
 template <int A, int MODE, int L>
 __global__ void __launch_bounds__(256) k_gnn(GnnArgs ga) {
   __shared__ float lds[L_TOTAL];
+  // the one-launch step's 1-D grid groups the workgroups by (net, share) combination k = b mod 8:
+  // blocks b = k mod 8 are dealt to one XCD, so a combination's 32 tiles share an L2 (gnn_tail)
+  int tile, net, zs;
+  if (MODE == GNN_GRAD && ga.xgrid) {
+    const int b = blockIdx.x;
+    tile = b >> 3; net = (b >> 2) & 1; zs = b & 3;
+  } else {
+    tile = blockIdx.x; net = blockIdx.y; zs = blockIdx.z;
+  }
   const int blk = blockIdx.x + gridDim.x * (blockIdx.y + 2 * blockIdx.z);
   if (MODE == GNN_GRAD) SPAN(0, blk, 0);
-  if (blockIdx.y == 0) gnn_tile<A, MODE, 0, L>(ga, lds);
-  else gnn_tile<A, MODE, 1, L>(ga, lds);
+  if (net == 0) gnn_tile<A, MODE, 0, L>(ga, lds, tile, zs);
+  else gnn_tile<A, MODE, 1, L>(ga, lds, tile, zs);
   if (MODE == GNN_GRAD) SPAN(0, blk, 1);
   (void)blk;
   if constexpr (MODE == GNN_GRAD)
-    if (ga.tail) gnn_tail(ga, reinterpret_cast<int*>(lds));
+    if (ga.tail) gnn_tail(ga, lds, tile, net, zs);
 }
 // k_gnn instance of a layer (MODE fixed)
 #define GNN_LAUNCH(MODE, L_, grid, s, ga)                                                            \
@@ -836,12 +833,12 @@ __global__ void __launch_bounds__(256) k_gnn(GnnArgs ga) {
 // ---- reduction over tiles: grad[p] = sum_t part[t][p] (fixed order) + norm^2 partials ----
 // loss statistics of the step: statp [net][tile][8]; lane j < 10 sums (net, stat) j over the
 // tiles (independent loads), lane 0 combines
-__device__ __forceinline__ void gnn_step_stats(const GnnArgs& ga, int ntiles, bool coh = false) {
+__device__ __forceinline__ void gnn_step_stats(const GnnArgs& ga, int ntiles) {
   __shared__ float sv[10];
   const int j = threadIdx.x, b = j / 5, k = j - 5 * b;
   float sv_t[DDRL_MB / 4];
 #pragma unroll
-  for (int t = 0; t < DDRL_MB / 4; ++t) sv_t[t] = t < ntiles ? cld(coh, ga.statp + (b * DDRL_MB / 4 + t) * 8 + k) : 0.f;
+  for (int t = 0; t < DDRL_MB / 4; ++t) sv_t[t] = t < ntiles ? ga.statp[(b * DDRL_MB / 4 + t) * 8 + k] : 0.f;
   float a = 0.f;
 #pragma unroll
   for (int t = 0; t < DDRL_MB / 4; ++t) a += sv_t[t];
@@ -864,39 +861,10 @@ __device__ __forceinline__ void gnn_step_stats(const GnnArgs& ga, int ntiles, bo
   }
 }
 
-// Bounded waits of the one-launch step (gnn_tail below): an arrival flag / a tagged granule.
-__device__ __forceinline__ bool gnn_wait_tag(const GnnArgs& ga, const unsigned* flag, unsigned long long t0) {
-  for (;;) {
-    if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ga.tag) return true;
-    const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
-    if (dt > 20000ull && __hip_atomic_load(ga.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
-    if (dt > 300000000ull) {   // 3 s
-      __hip_atomic_store(ga.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-__device__ __forceinline__ float gnn_wait_gran(const GnnArgs& ga, const unsigned long long* g, unsigned long long t0,
-                                               bool& ok) {
-  for (;;) {
-    const unsigned long long v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if ((unsigned)(v >> 32) == ga.tag) return __uint_as_float((unsigned)v);
-    const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
-    if ((dt > 20000ull && __hip_atomic_load(ga.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) || dt > 300000000ull) {
-      __hip_atomic_store(ga.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      ok = false;
-      return 0.f;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
 // ---- reduction over tiles: grad[p] = sum_t part[t][p] (fixed order) + norm^2 partials ----
 // Reduction block b (256 parameters): this thread's summed gradient (parameter b * 256 + tid) is
-// returned; the block's squared-norm partial goes to normp[b] (coh: the tagged granule gran[b]).
-__device__ __forceinline__ float gnn_reduce_block(const GnnArgs& ga, int b, int ntiles, int n, bool store_grad,
-                                                  bool coh = false) {
+// returned; the block's squared-norm partial goes to normp[b].
+__device__ __forceinline__ float gnn_reduce_block(const GnnArgs& ga, int b, int ntiles, int n, bool store_grad) {
   __shared__ float red[4];
   const int p = b * 256 + threadIdx.x;
   // all tile partials of this parameter in flight at once (a runtime-bound loop would wait
@@ -904,7 +872,7 @@ __device__ __forceinline__ float gnn_reduce_block(const GnnArgs& ga, int b, int 
   float v[DDRL_MB / 4];
 #pragma unroll
   for (int t = 0; t < DDRL_MB / 4; ++t)
-    v[t] = (p < n && t < ntiles) ? cld(coh, ga.part + (size_t)t * ga.part_stride + p) : 0.f;
+    v[t] = (p < n && t < ntiles) ? ga.part[(size_t)t * ga.part_stride + p] : 0.f;
   float s = 0.f;
 #pragma unroll
   for (int t = 0; t < DDRL_MB / 4; ++t) s += v[t];
@@ -912,25 +880,16 @@ __device__ __forceinline__ float gnn_reduce_block(const GnnArgs& ga, int b, int 
   float ss = wave_sum(s * s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const float np = ((red[0] + red[1]) + red[2]) + red[3];
-    if (coh)
-      __hip_atomic_store(ga.gran + b, ((unsigned long long)ga.tag << 32) | __float_as_uint(np), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    else
-      ga.normp[b] = np;
-  }
+  if (threadIdx.x == 0) ga.normp[b] = ((red[0] + red[1]) + red[2]) + red[3];
   return p < n ? s : 0.f;
 }
 
 // ---- tf.clip_by_global_norm + tf1 Adam on the 256 parameters of block b ----
 // g0, mi, vi, th0: this thread's gradient and state (loaded by the caller, ahead of the norm it
-// waits on); b1p, b2p: the step's beta powers.  coh: the norm^2 partials are the tagged
-// granules of this launch's reduction blocks (waited for, bounded; false = abandoned).
-__device__ __forceinline__ bool gnn_adam_block(const GnnArgs& ga, int b, int nred, int n, float g0, float mi,
-                                               float vi, float th0, float b1p, float b2p, bool coh = false) {
+// waits on); b1p, b2p: the step's beta powers.
+__device__ __forceinline__ void gnn_adam_block(const GnnArgs& ga, int b, int nred, int n, float g0, float mi,
+                                               float vi, float th0, float b1p, float b2p) {
   __shared__ float scale_s;
-  __shared__ int ok_s;
   const UpdateArgs& U = ga.u;
   const UpdateHyper& h = ga.h;
   const int p = b * 256 + threadIdx.x;
@@ -938,16 +897,12 @@ __device__ __forceinline__ bool gnn_adam_block(const GnnArgs& ga, int b, int nre
   if (threadIdx.x < 64) {
     // squared-norm partials of the reduction blocks: the same butterfly in every block
     float part = 0.f;
-    bool ok = true;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    for (int k = threadIdx.x; k < nred; k += 64) part += coh ? gnn_wait_gran(ga, ga.gran + k, t0, ok) : ga.normp[k];
+    for (int k = threadIdx.x; k < nred; k += 64) part += ga.normp[k];
     const float tot = wave_sum(part);
-    ok = __all(ok);
     if (threadIdx.x != 0) goto done;
-    ok_s = ok;
     const float gn = sqrtf(tot);
     scale_s = h.grad_clip * fminf(1.f / gn, 1.f / h.grad_clip);
-    if (b == 0 && ok) {
+    if (b == 0) {
       if (U.stats) {
         U.stats[(size_t)ga.step * 8 + 6] = gn;
         U.stats[(size_t)ga.step * 8 + 7] = scale_s;
@@ -958,8 +913,7 @@ __device__ __forceinline__ bool gnn_adam_block(const GnnArgs& ga, int b, int nre
   }
 done:
   __syncthreads();
-  if (!ok_s) return false;
-  if (!pv) return true;
+  if (!pv) return;
   const float alpha = h.lr * sqrtf(1.f - b2p) / (1.f - b1p);
   const float g = g0 * scale_s;
   mi = mi + (g - mi) * (1.f - h.b1);
@@ -967,7 +921,6 @@ done:
   U.m[p] = mi;
   U.v[p] = vi;
   U.theta[p] = th0 - (mi * alpha) / (sqrtf(vi) + h.eps);
-  return true;
 }
 
 // Three-launch step: the last block of the reduction grid (one past the parameter blocks) sums
@@ -996,7 +949,7 @@ __global__ void __launch_bounds__(256) k_gnn_adam(GnnArgs ga, int nred, int n) {
   const float g0 = pv ? ga.grad[p] : 0.f;
   const float mi = pv ? U.m[p] : 0.f, vi = pv ? U.v[p] : 0.f;
   const float th0 = pv ? U.theta[p] : 0.f;
-  (void)gnn_adam_block(ga, blockIdx.x, nred, n, g0, mi, vi, th0, ga.bp_cur[0], ga.bp_cur[1]);
+  gnn_adam_block(ga, blockIdx.x, nred, n, g0, mi, vi, th0, ga.bp_cur[0], ga.bp_cur[1]);
   RSTAMPB(blockIdx.x, 3);
   SPAN(2, blockIdx.x, 1);
 }
@@ -1004,67 +957,184 @@ __global__ void __launch_bounds__(256) k_gnn_adam(GnnArgs ga, int nred, int n) {
 // ---- one-launch step: the reduction and Adam run in the gradient launch's tail ----
 // The reduction needs every tile's partials and Adam the global norm, so the step used to be
 // three launches (two kernel boundaries of ~1.5-2 us each, MI355X_MICROARCH.md "boundary").
-// Here the first nred + 1 workgroups of the gradient grid (linear block id b) are also the
-// reduction blocks (b = nred sums the loss statistics).  Every workgroup, once its partials and
-// statistics are written, raises its arrival flag (flag[block] = this launch's tag); a
-// reduction block, after its own tile, waits until every flag carries the tag (one flag per
-// thread), runs the reduction block's code, publishes its norm^2 partial as a tagged granule
-// {value, tag}, waits for the granules of all nred blocks (the same butterfly order as
-// k_gnn_adam) and runs the Adam block's code on its 256 parameters.  Same blocks, same order of
-// every sum as the three-launch step: bit-identical results (tests/test_gpu_gnn.py).
-// Protocol: every value another workgroup reads (partials, loss statistics, flags, granules) is
-// a relaxed device-scope atomic store (sc1: written through to the device's coherence point)
-// and load; a flag or granule is written only after an s_waitcnt on the stores it covers.  No
-// read-modify-write counter: 256 arrivals on one device-scope atomic serialize at ~12 ns each
-// (MI355X_MICROARCH.md "fanin"), measured 22.7 us per step against 18.9 for three launches, and
-// release / acquire orderings (an L2 write-back per arrival, an L2 invalidate per poll) 33.1.
-// The waiting workgroups wait only on workgroups of the same grid, at most one per CU, so all
-// are resident; every wait is bounded (the error word, as the fcnet exchanges; the host
-// restores its snapshot).
-__device__ __forceinline__ void gnn_tail(const GnnArgs& ga, int* bsh) {
-  const int ngrid = (int)(gridDim.x * gridDim.y * gridDim.z);
-  const int b = (int)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z));
-  // every wave's partial and statistics stores have completed before the flag goes up
-  __builtin_amdgcn_s_waitcnt(0);
+// The one-launch step keeps the reduction inside an XCD: the gradient grid is 1-D, block
+// b = 8 tile + k with k = 4 net + share, so the 32 tiles of one (net, backward share)
+// combination k are blocks b = k mod 8, which the dispatcher deals to one XCD (the fcnet row
+// split relies on the same rule, with its placement check).  Every parameter's partials come
+// from one share (the owner lists plist, found once per context by gnn_build_owner_lists), so a
+// combination's partials are all written -- plain stores into the XCD's L2 -- and read on one
+// XCD:
+//   * each workgroup, once its partials and loss statistics are in L2 (s_waitcnt), raises its
+//     arrival flag (flag[b] = this launch's tag);
+//   * tiles r < R_k of combination k are also its reduction blocks: reducer r waits for the 32
+//     flags of its combination (one per thread, sc1 polls: they miss the CU's own L1), sums
+//     the 32 partials of 256 owned parameters in tile order with sc1 loads (the three-launch
+//     reduction's order, so the gradient is bit-identical) and publishes its norm^2 partial as
+//     a tagged granule {value, tag} with a device-scope atomic store (the one value that crosses
+//     XCDs);
+//   * every reducer waits for all granules, forms the global norm in one fixed order and runs
+//     clip + tf1 Adam on its 256 parameters; global reducer 0 writes the norm statistics and the
+//     next beta powers (read by every reducer before its granule goes up);
+//   * tile R_k of combination (net, 0) sums that net's loss statistics.
+// Waits are bounded (the error word, as the fcnet exchanges; the host restores its snapshot and
+// the context goes on with three launches).  Measured first with device-wide protocols instead:
+// every partial written through to memory + one arrival counter 22.7 us per step (256 arrivals
+// on one device-scope atomic serialize, MI355X_MICROARCH.md "fanin"), flags 21.5, release /
+// acquire 33.1, against 18.9 for three launches.
+__device__ __forceinline__ bool gnn_wait_flag(const GnnArgs& ga, const unsigned* flag, unsigned long long t0) {
+  for (;;) {
+    if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ga.tag) return true;
+    const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
+    if ((dt > 20000ull && __hip_atomic_load(ga.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) || dt > 300000000ull) {
+      __hip_atomic_store(ga.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+__device__ __forceinline__ bool gnn_wait_gran(const GnnArgs& ga, const unsigned long long* g, unsigned long long t0,
+                                              float& out) {
+  for (;;) {
+    const unsigned long long v = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((unsigned)(v >> 32) == ga.tag) {
+      out = __uint_as_float((unsigned)v);
+      return true;
+    }
+    const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
+    if ((dt > 20000ull && __hip_atomic_load(ga.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) || dt > 300000000ull) {
+      __hip_atomic_store(ga.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+__device__ __forceinline__ float sc1_ld(const float* p) {
+  return __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+__device__ __forceinline__ void gnn_tail(const GnnArgs& ga, float* lds, int tile, int net, int zs) {
+  const int b = blockIdx.x, k = b & 7, tid = threadIdx.x;
+  // LDS of the finished tile, reused: [0..3] norm^2 of the waves, [4..5] beta powers,
+  // [8..12] loss statistics, [16] clip scale, [17] ok, [64 ..] granule values
+  float* T = lds;
+  __builtin_amdgcn_s_waitcnt(0);   // this wave's partial / statistics stores are in L2
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(ga.flags + b, ga.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (b > ga.nred) return;
-  // a reduction block: every workgroup of the grid has arrived (one flag per thread)
+  if (tid == 0) __hip_atomic_store(ga.flags + b, ga.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const int m = ga.poff[k + 1] - ga.poff[k];
+  const int r = tile;   // reducer r of combination k: parameters plist[poff[k] + 256 r ..]
+  const int R = (m + 255) / 256;
+  const UpdateArgs& U = ga.u;
+  // the first tile after the reducers of combination (net, 0) sums that net's loss statistics
+  // (the three-launch order), off the reducers' path
+  const bool stats = zs == 0 && r == R && U.stats;
+  if (r > R || (r == R && !stats)) return;
+  const bool adam = U.grad_out == nullptr;
+  // this thread's parameter and its state (the loads overlap the flag wait)
+  const int e = 256 * r + tid;
+  const bool pv = !stats && e < m;
+  const int p = pv ? ga.plist[ga.poff[k] + e] : 0;
+  const float mi = pv && adam ? U.m[p] : 0.f, vi = pv && adam ? U.v[p] : 0.f;
+  const float th0 = pv && adam ? U.theta[p] : 0.f;
+  if (tid == 0 && adam && !stats) {
+    T[4] = U.beta_pow[0];
+    T[5] = U.beta_pow[1];
+  }
+  // the combination's 32 workgroups have arrived (one flag per thread)
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  const bool ok = (int)threadIdx.x >= ngrid || gnn_wait_tag(ga, ga.flags + threadIdx.x, t0);
+  const bool ok = tid >= ga.ntiles || gnn_wait_flag(ga, ga.flags + 8 * tid + k, t0);
   if (!__syncthreads_and(ok)) return;
-  RSTAMPB(b, 0);
-  SPAN(1, b, 0);
-  if (b == ga.nred) {   // the loss statistics of the step
-    if (threadIdx.x < 10) gnn_step_stats(ga, ga.ntiles, true);
-    SPAN(1, b, 1);
+  if (stats) {
+    if (tid < 5) {   // all 32 loads in flight, then summed in tile order
+      float sv[DDRL_MB / 4];
+#pragma unroll
+      for (int t = 0; t < DDRL_MB / 4; ++t)
+        sv[t] = t < ga.ntiles ? sc1_ld(ga.statp + (net * (DDRL_MB / 4) + t) * 8 + tid) : 0.f;
+      float a = 0.f;
+#pragma unroll
+      for (int t = 0; t < DDRL_MB / 4; ++t) a += sv[t];
+      T[8 + tid] = a;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const float nr = (float)ga.n_graphs;
+      float* so = U.stats + (size_t)ga.step * 8;
+      if (net == 0) {
+        so[1] = T[8] / nr; so[3] = T[9] / nr; so[4] = T[10] / nr;
+      } else {
+        so[2] = T[8] / nr;
+        const float vy = T[10] / nr - (T[9] / nr) * (T[9] / nr);
+        const float vd = T[12] / nr - (T[11] / nr) * (T[11] / nr);
+        so[5] = vy > 0.f ? fmaxf(-1.f, 1.f - vd / vy) : 0.f;
+      }
+    }
     return;
   }
-  const UpdateArgs& U = ga.u;
-  const int n = ga.n_params;
-  // the parameter state first (its loads overlap the partials'), and the beta powers: read by
-  // thread 0 and landed before this block's granule goes up below (block 0 writes the next beta
-  // powers only once every granule is there)
-  const int p = b * 256 + threadIdx.x;
-  const bool pv = p < n && !U.grad_out;
-  const float mi = pv ? U.m[p] : 0.f, vi = pv ? U.v[p] : 0.f;
-  const float th0 = pv ? U.theta[p] : 0.f;
-  float* bps = reinterpret_cast<float*>(bsh);
-  if (threadIdx.x == 0 && !U.grad_out) {
-    bps[0] = U.beta_pow[0];
-    bps[1] = U.beta_pow[1];
-    __builtin_amdgcn_s_waitcnt(0);
+  RSTAMPB(ga.rbase[k] + r, 0);
+  SPAN(1, ga.rbase[k] + r, 0);
+  // the reduction: 32 partials of this thread's parameter, in tile order
+  float v[DDRL_MB / 4];
+#pragma unroll
+  for (int t = 0; t < DDRL_MB / 4; ++t)
+    v[t] = (pv && t < ga.ntiles) ? sc1_ld(ga.part + (size_t)t * ga.part_stride + p) : 0.f;
+  float g0 = 0.f;
+#pragma unroll
+  for (int t = 0; t < DDRL_MB / 4; ++t) g0 += v[t];
+  if (!adam) {   // data-parallel gradient: the all-reduce and Adam follow as launches
+    if (pv) ga.grad[p] = g0;
+    return;
   }
-  const float g0 = gnn_reduce_block(ga, b, ga.ntiles, n, U.grad_out != nullptr, true);   // syncs
-  RSTAMPB(b, 1);
-  SPAN(1, b, 1);
-  if (U.grad_out) return;   // data-parallel gradient: the all-reduce and Adam follow as launches
-  const float b1p = bps[0], b2p = bps[1];
-  RSTAMPB(b, 2);
-  SPAN(2, b, 0);
-  (void)gnn_adam_block(ga, b, ga.nred, n, g0, mi, vi, th0, b1p, b2p, true);
-  RSTAMPB(b, 3);
-  SPAN(2, b, 1);
+  const float ss = wave_sum(g0 * g0);
+  if ((tid & 63) == 0) T[tid >> 6] = ss;
+  __syncthreads();
+  const int gi = ga.rbase[k] + r;   // global reducer index
+  if (tid == 0) {
+    __builtin_amdgcn_s_waitcnt(0);   // the beta powers above have landed before the granule goes up
+    const float np = ((T[0] + T[1]) + T[2]) + T[3];
+    __hip_atomic_store(ga.gran + gi, ((unsigned long long)ga.tag << 32) | __float_as_uint(np), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  RSTAMPB(gi, 1);
+  SPAN(1, gi, 1);
+  // every reducer's norm^2 partial (one granule per thread), then the norm in a fixed order
+  const int nr_all = ga.rbase[8];
+  float gv = 0.f;
+  const bool ok2 = tid >= nr_all || gnn_wait_gran(ga, ga.gran + tid, t0, gv);
+  T[64 + tid] = gv;
+  if (!__syncthreads_and(ok2)) return;
+  RSTAMPB(gi, 2);
+  SPAN(2, gi, 0);
+  const UpdateHyper& h = ga.h;
+  const float b1p = T[4], b2p = T[5];
+  if (tid < 64) {
+    float part = 0.f;
+    for (int j = tid; j < nr_all; j += 64) part += T[64 + j];
+    const float tot = wave_sum(part);
+    if (tid == 0) {
+      const float gn = sqrtf(tot);
+      const float scale = h.grad_clip * fminf(1.f / gn, 1.f / h.grad_clip);
+      T[16] = scale;
+      if (gi == 0) {
+        if (U.stats) {
+          U.stats[(size_t)ga.step * 8 + 6] = gn;
+          U.stats[(size_t)ga.step * 8 + 7] = scale;
+        }
+        U.beta_pow[0] = b1p * h.b1;
+        U.beta_pow[1] = b2p * h.b2;
+      }
+    }
+  }
+  __syncthreads();
+  if (pv) {
+    const float alpha = h.lr * sqrtf(1.f - b2p) / (1.f - b1p);
+    const float g = g0 * T[16];
+    const float m1 = mi + (g - mi) * (1.f - h.b1);
+    const float v1 = vi + (g * g - vi) * (1.f - h.b2);
+    U.m[p] = m1;
+    U.v[p] = v1;
+    U.theta[p] = th0 - (m1 * alpha) / (sqrtf(v1) + h.eps);
+  }
+  RSTAMPB(gi, 3);
+  SPAN(2, gi, 1);
 }
 
 // Pre-gather of a run of minibatch steps: dst[k][i][col] = rec[shuffle[perm[e][b] * 128 + i]][col]
@@ -1119,32 +1189,90 @@ void launch_forward_gnn(hipStream_t s, const ForwardArgs& fa, int layer) {
   GNN_LAUNCH(GNN_FWD, layer, dim3((fa.n + 3) / 4, 2), s, ga);
 }
 
-void launch_step_gnn(hipStream_t s, const UpdateArgs& u, const UpdateHyper& h, int step, int nrows, float inv_n,
-                     GnnScratch& sc, const float* stage, int layer) {
-  check_a(u.A);
+static GnnArgs grad_args(const UpdateArgs& u, const UpdateHyper& h, int step, int nrows, float inv_n,
+                         const GnnScratch& sc, const float* stage, int layer) {
   GnnArgs ga{};
   ga.theta = u.theta; ga.u = u; ga.h = h; ga.step = step; ga.n_graphs = nrows; ga.inv_n = inv_n;
   ga.part = sc.part; ga.part_stride = sc.part_stride; ga.statp = sc.statp; ga.normp = sc.normp;
   ga.bp_cur = sc.bp_cur; ga.grad = u.grad_out ? u.grad_out : sc.grad;
   ga.stage = stage;
-  const int ntiles = (nrows + 3) / 4;
-  const int n = gnn_param_total(u.A, layer);
-  const int nred = (n + 255) / 256;
-  const int ngrid = ntiles * 2 * GNN_Z;
-  ga.ntiles = ntiles; ga.n_params = n; ga.nred = nred; ga.err = sc.err; ga.flags = sc.flags; ga.gran = sc.gran;
-  // one launch per step when the gradient grid can host the nred + 1 reduction blocks (and every
-  // workgroup one flag per reduction-block thread)
-  ga.tail = sc.tail && sc.flags && ngrid >= nred + 1 && ngrid <= 256;
+  ga.ntiles = (nrows + 3) / 4;
+  ga.n_params = gnn_param_total(u.A, layer);
+  ga.nred = (ga.n_params + 255) / 256;
+  ga.err = sc.err; ga.flags = sc.flags; ga.gran = sc.gran;
+  ga.only_share = -1;
+  return ga;
+}
+
+// Owner lists of the one-launch step: which backward share writes each parameter's partials
+// (the gradient kernel's own store pattern -- gnn_tile_owner, gnn_hbwd_owner, share 0 for the
+// head and attention vectors -- observed, not restated): one gradient launch per share with the
+// other shares idle, over a partial row pre-filled with a NaN pattern no computed value has.
+// Every parameter must be owned by exactly one share, and each (net, share) combination's list
+// must fit the reducers its 32 tiles provide; otherwise the context keeps three launches.
+static void gnn_build_owner_lists(hipStream_t s, const UpdateArgs& u, const UpdateHyper& h, float inv_n,
+                                  GnnScratch& sc, int layer) {
+  sc.lists = -1;
+  GnnArgs ga = grad_args(u, h, 0, 4, inv_n, sc, nullptr, layer);
+  const int n = ga.n_params;
+  const int actor = gnn_net_off(u.A, 1, layer).wenc;   // first critic parameter
+  std::vector<int> own(n, -1);
+  std::vector<unsigned> row(n);
+  for (int z = 0; z < GNN_Z; ++z) {
+    if (hipMemsetD32Async((hipDeviceptr_t)sc.part, 0xFFFFFFFFu, (size_t)n, s) != hipSuccess) return;
+    ga.only_share = z;
+    GNN_LAUNCH(GNN_GRAD, layer, dim3(1, 2, GNN_Z), s, ga);
+    if (hipMemcpyAsync(row.data(), sc.part, (size_t)n * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+      return;
+    for (int p = 0; p < n; ++p) {
+      if (row[p] == 0xFFFFFFFFu) continue;
+      if (own[p] >= 0) return;   // two shares write one parameter
+      own[p] = z;
+    }
+  }
+  std::vector<int> lst;
+  int poff[9], rbase[9];
+  poff[0] = rbase[0] = 0;
+  for (int k = 0; k < 8; ++k) {
+    const int net = k >> 2, z = k & 3;
+    for (int p = 0; p < n; ++p) {
+      if (own[p] < 0) return;   // a parameter no share writes
+      if ((p >= actor) == (net == 1) && own[p] == z) lst.push_back(p);
+    }
+    poff[k + 1] = (int)lst.size();
+    const int R = (poff[k + 1] - poff[k] + 255) / 256;
+    if (R >= DDRL_MB / 4) return;   // the reducers and the statistics tile need R + 1 <= 32 tiles
+    rbase[k + 1] = rbase[k] + R;
+  }
+  if ((int)lst.size() != n || rbase[8] > 256) return;
+  if (hipMemcpy(sc.plist, lst.data(), (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess) return;
+  for (int k = 0; k < 9; ++k) sc.poff[k] = poff[k], sc.rbase[k] = rbase[k];
+  sc.lists = 1;
+}
+
+void launch_step_gnn(hipStream_t s, const UpdateArgs& u, const UpdateHyper& h, int step, int nrows, float inv_n,
+                     GnnScratch& sc, const float* stage, int layer) {
+  check_a(u.A);
+  GnnArgs ga = grad_args(u, h, step, nrows, inv_n, sc, stage, layer);
+  const int ntiles = ga.ntiles, n = ga.n_params, nred = ga.nred;
+  // one launch per step for full 128-row minibatches (32 tiles per combination)
+  if (sc.tail && sc.lists == 0 && ntiles == DDRL_MB / 4 && GNN_Z == 4) gnn_build_owner_lists(s, u, h, inv_n, sc, layer);
+  ga.tail = sc.tail && sc.lists == 1 && ntiles == DDRL_MB / 4 && GNN_Z == 4;
   if (ga.tail) {
     if (++sc.seq == 0) sc.seq = 1;   // tags never 0 (the buffers start zeroed)
     ga.tag = sc.seq;
+    ga.xgrid = 1;
+    ga.plist = sc.plist;
+    for (int k = 0; k < 9; ++k) ga.poff[k] = sc.poff[k], ga.rbase[k] = sc.rbase[k];
+    GNN_LAUNCH(GNN_GRAD, layer, dim3(ntiles * 8), s, ga);
+    return;
   }
   // tiles of the critic write their statistics after the actor's: statp [2][32][8]
   GNN_LAUNCH(GNN_GRAD, layer, dim3(ntiles, 2, GNN_Z), s, ga);
 #ifdef DDRL_ABL_GNN_GRAD_ONLY   // ablation build (timing only): no reduction / Adam launches
   return;
 #endif
-  if (ga.tail) return;
   hipLaunchKernelGGL(k_gnn_reduce, dim3(nred + 1), dim3(256), 0, s, ga, ntiles, n);
   if (!u.grad_out) hipLaunchKernelGGL(k_gnn_adam, dim3(nred), dim3(256), 0, s, ga, nred, n);
 }

@@ -189,8 +189,11 @@ struct GnnArgs {
   // staged minibatch (fused update only): the records of this step, contiguous [128][stride]
   // (a slot of the pre-gathered chunk); null: gather through shuffle / perm
   const float* stage;
-  // one-launch step (gnn.hip gnn_tail): arrival flags [256], norm^2 granules [256], this launch's tag
+  // one-launch step (gnn.hip gnn_tail): arrival flags [256], norm^2 granules [256], this launch's
+  // tag; the XCD-grouped 1-D grid (xgrid); the parameters of each (net, share) combination
+  // (plist[poff[k] .. poff[k + 1]), k = 4 net + share) and the first reducer index of each (rbase)
   unsigned* flags; unsigned long long* gran; unsigned tag; int tail; int nred; int n_params; int ntiles; int* err;
+  int xgrid; int only_share; const int* plist; int poff[9]; int rbase[9];
 };
 struct GnnScratch {
   float* part; int part_stride; float* statp; float* normp; float* bp_cur; float* grad;
@@ -199,6 +202,9 @@ struct GnnScratch {
   unsigned* flags;              // [256] arrival flags of the one-launch step (device)
   unsigned long long* gran;     // [256] tagged norm^2 partials {value, tag} of its reduction blocks
   unsigned seq;                 // tag of the last one-launch step (host; never 0)
+  int* plist;                   // [n_params] parameters by (net, share) owner (device)
+  int poff[9], rbase[9];        // list offsets / first reducer of each combination
+  int lists;                    // 0: not built yet, 1: built, -1: unusable (three launches)
   int tail;           // 1: reduction + clip + Adam in the gradient launch (DDRL_GNN_TAIL, default 1)
   int* err;           // the context's error word
 };

@@ -224,16 +224,18 @@ def test_gnn_update_across_record_chunks():
     ctx.close()
 
 
-def test_gnn_one_launch_step_equals_three_launch_step(monkeypatch):
-    """Round 4: the GNN training step in ONE launch (the reduction and clip + Adam run in the
-    gradient launch's tail, by its last-arriving workgroups; gnn.hip gnn_tail) is bit-identical to
-    the three-launch step (DDRL_GNN_TAIL=0: k_gnn -> k_gnn_reduce -> k_gnn_adam) over the whole
-    100-step schedule: parameters, Adam m / v, beta powers and every step's learner statistics.
-    Also the data-parallel gradient (ddrl_ppo_grad of 128 rows: reduction in the tail, Adam left
-    to the caller) against the three-launch gradient."""
+def test_gnn_one_launch_step_matches_three_launch_step(monkeypatch):
+    """Round 4: the GNN training step in ONE launch (gnn.hip gnn_tail: the 32 tiles of each
+    (net, backward share) combination on one XCD reduce their partials through its L2, then a
+    tagged norm^2 granule per reducer crosses XCDs, then clip + Adam) against the three-launch
+    step (DDRL_GNN_TAIL=0: k_gnn -> k_gnn_reduce -> k_gnn_adam).  The gradient of a minibatch
+    (ddrl_ppo_grad of 128 rows: the reduction in the tail, Adam left to the caller) is bit-identical
+    -- every parameter's 32 partials are summed in the same tile order.  The global norm sums
+    the same squares in another grouping, so the 100-step schedule agrees to fp32 rounding of the
+    clip scale: parameters within 2e-6, learner statistics within 1e-5 relative + 2e-6; both paths are
+    held to the fp64 oracle by the other tests of this file."""
     import torch
     from ddrl_amd import native as N
-    layer = "mpnn"   # the tail runs after the layer code, the same for every layer
     ctx0, cfg, orc, norms, params, _, _ = _rollout(32, 10, 81, head_scale=1.0)
     ctx0.close()
     ctxs = []
@@ -244,7 +246,7 @@ def test_gnn_one_launch_step_equals_three_launch_step(monkeypatch):
         rec = orc.flat_records(0, lay)
         c.records_set(0, rec)
         c.adv_norm_set(0, *norms[0])
-        c.params_set(0, O.pack(params, O.gnn_param_shapes(4, layer=layer)))
+        c.params_set(0, O.pack(params, SHAPES))
         ctxs.append(c)
     monkeypatch.delenv("DDRL_GNN_TAIL")
     sh, pe = O.sgd_schedule(np.random.default_rng(17), rec.shape[0], 128, cfg.num_sgd_iter)
@@ -259,14 +261,14 @@ def test_gnn_one_launch_step_equals_three_launch_step(monkeypatch):
         c.ppo_update(1, [torch.from_numpy(sh).cuda()], [torch.from_numpy(pe).cuda()], [0.2])
         c.synchronize()
     np.testing.assert_array_equal(grads[0], grads[1])
+    assert np.abs(grads[0]).max() > 0
     a, b = ctxs
-    np.testing.assert_array_equal(a.params_get(0), b.params_get(0))
+    pa, pb = a.params_get(0), b.params_get(0)
+    assert not np.array_equal(pa, O.pack(params, SHAPES))
+    np.testing.assert_allclose(pa, pb, rtol=0, atol=2e-6)
     ma, va, b1a, b2a = a.adam_get(0)
     mb, vb, b1b, b2b = b.adam_get(0)
-    np.testing.assert_array_equal(ma, mb)
-    np.testing.assert_array_equal(va, vb)
     assert (b1a, b2a) == (b1b, b2b)
-    np.testing.assert_array_equal(a.ppo_stats(0, steps), b.ppo_stats(0, steps))
-    assert not np.array_equal(a.params_get(0), O.pack(params, O.gnn_param_shapes(4, layer=layer)))
+    np.testing.assert_allclose(a.ppo_stats(0, steps), b.ppo_stats(0, steps), rtol=1e-5, atol=2e-6)
     for c in ctxs:
         c.close()

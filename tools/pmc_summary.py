@@ -33,6 +33,7 @@ import sys
 
 GFX950_FETCH_CORRECTION = 2.0
 N_SIMD = 1024
+LONG_CLOCK_GHZ = 2.39   # set from the local / c4 update dispatches in main()
 WORKLOADS = {
     "local": {"kernels": ["void k_update_ffn<2, 9"], "steps": 10 * 6400 * 4,
               "workload": "QuantrupedMultiEnv_Local, 4096 envs, T=200 (one fused launch: 10 x 6400 steps x 4 policies)",
@@ -47,7 +48,9 @@ WORKLOADS = {
     "c5": {"kernels": ["void k_gnn<2, 2", "k_gnn_reduce", "k_gnn_adam", "k_gnn_gather"], "steps": 10 * 800,
            "workload": "QuantrupedMultiEnv_DecentralShared_Graph, 128 envs, T=200 (10 x 800 steps, 3 launches "
                        "each, plus one record gather per 1024 steps)",
-           "mfma": {"kernel": "void k_gnn<2, 2", "active_simds": 1024, "flop_per_step": None},
+           # gradient launch: 32 tiles x 2 nets x 4 backward shares x 4 waves; FLOP: bench.py
+           # gnn_flops_per_row(2) x 128 rows (the forward counted once, not once per share)
+           "mfma": {"kernel": "void k_gnn<2, 2", "active_simds": 1024, "flop_per_step": 764800 * 128},
            "also": ["void k_gnn<2, 0"]},
 }
 
@@ -68,7 +71,7 @@ def counter(path, name, prefix):
     return tot, n
 
 
-def mfma_stats(d, prefix, active_simds, flop_per_dispatch=None):
+def mfma_stats(d, prefix, active_simds, flop_total=None):
     """Matrix-core busy and clock of the dispatches of one kernel in pass directory d."""
     cpath = os.path.join(d, "run_counter_collection.csv")
     tpath = os.path.join(d, "run_kernel_trace.csv")
@@ -97,19 +100,33 @@ def mfma_stats(d, prefix, active_simds, flop_per_dispatch=None):
     cyc = tot.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
     busy = tot.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
     ns = tot.get("ns", 0.0)
+    # GRBM_GUI_ACTIVE / duration reads high on dispatches shorter than ~0.3 ms (the guide); for
+    # those the kernel cycles are the trace duration at the clock of the long update dispatches
+    # (LONG_CLOCK_GHZ, measured on the 0.7-2.7 s fcnet update launches of the same run)
+    short = len(per) and ns / len(per) < 1e6
+    if short and ns > 0:
+        cyc = ns * LONG_CLOCK_GHZ
     out = {"kernel": prefix, "dispatches": len(per), "duration_ns": ns, "kernel_cycles": cyc,
+           "cycles_source": ("trace duration x %.3f GHz (dispatches < 1 ms: GRBM_GUI_ACTIVE reads high)" % LONG_CLOCK_GHZ
+                             if short else "GRBM_GUI_ACTIVE / 8"),
            "SQ_VALU_MFMA_BUSY_CYCLES": busy, "SQ_BUSY_CYCLES": tot.get("SQ_BUSY_CYCLES"),
            "SQ_WAVE_CYCLES": tot.get("SQ_WAVE_CYCLES"), "GRBM_GUI_ACTIVE": tot.get("GRBM_GUI_ACTIVE"),
-           "clock_ghz": cyc / ns if ns > 0 else None,
+           "clock_ghz": (tot.get("GRBM_GUI_ACTIVE", 0.0) / 8.0) / ns if ns > 0 and not short else None,
            "mfma_busy_frac_chip": busy / (cyc * N_SIMD) if cyc > 0 else None,
            "active_simds": active_simds,
            "mfma_busy_frac_of_active_simds": busy / (cyc * active_simds) if cyc > 0 and active_simds else None}
-    if flop_per_dispatch and busy > 0:
-        out["mfma_flop_per_busy_cycle_per_simd"] = flop_per_dispatch * len(per) / busy
+    if flop_total and busy > 0:
+        out["mfma_flop_per_busy_cycle_per_simd"] = flop_total / busy
     return out
 
 
 def main(d):
+    global LONG_CLOCK_GHZ
+    for name in ("local", "c4"):   # the clock the chip holds under the long update launches
+        st = mfma_stats(os.path.join(d, f"pmc_{name}_MFMA"), WORKLOADS[name]["mfma"]["kernel"], 1)
+        if st and st.get("clock_ghz"):
+            LONG_CLOCK_GHZ = st["clock_ghz"]
+            break
     out = {"command": "tools/profile_r04.sh: rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | "
                       "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE (separate passes, "
                       "--kernel-trace) -- python3 bench.py --steps 1 --warmup 0 ...",
@@ -130,7 +147,7 @@ def main(d):
                "hbm_bytes_per_step": round(total / w["steps"], 1)}
         m = w["mfma"]
         mdir = os.path.join(d, f"pmc_{name}_MFMA")
-        flop = m["flop_per_step"] * w["steps"] if m["flop_per_step"] and name != "c5" else None
+        flop = m["flop_per_step"] * w["steps"] if m["flop_per_step"] else None
         st = mfma_stats(mdir, m["kernel"], m["active_simds"], flop)
         if st is not None:
             res["mfma"] = st
