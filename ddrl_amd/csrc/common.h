@@ -72,9 +72,6 @@ __device__ __forceinline__ floatx4 splat4(float v) { floatx4 r = {v, v, v, v}; r
 // instructions, absolute error ~1.5e-7 everywhere (no cancellation guard near 0 is needed at
 // the 1e-5 parity bar: the error is absolute, like fp32 rounding of O(1) values); the
 // saturated ends come out exactly: 2^(+inf) -> rcp 0 -> -1, 2^(-inf) -> 2 - 1 = 1.
-#ifndef DDRL_FWD_INTERLEAVE
-#define DDRL_FWD_INTERLEAVE 1
-#endif
 __device__ __forceinline__ float tanh_fast(float x) {
 #ifdef DDRL_ABL_NO_TANH   // ablation build (timing only)
   return x * 0.5f;
@@ -261,13 +258,10 @@ __device__ __forceinline__ void ffn_fwd_rt(const NetLds& W, const float (*xop)[1
   float wq[3][4];
   ld2(0, wq[0]);
   ld2(1, wq[1]);
-  // Layer 2's k-step k = 4 fb + r takes layer 1's feature block fb: only block 0 is activated
-  // before the first MFMA; block fb + 1's four tanh run one per k-step in the shadow of block
-  // fb's MFMAs (independent of them; the same operations, so the same bits).
 #pragma unroll
   for (int t = 0; t < RT; ++t)
 #pragma unroll
-    for (int ob = 0; ob < (DDRL_FWD_INTERLEAVE ? 1 : 4); ++ob)
+    for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
       for (int r = 0; r < 4; ++r) h1[t][ob][r] = tanh_fast(h1[t][ob][r]);
 
@@ -286,9 +280,6 @@ __device__ __forceinline__ void ffn_fwd_rt(const NetLds& W, const float (*xop)[1
       for (int ob = 0; ob < 4; ++ob)
 #pragma unroll
         for (int t = 0; t < RT; ++t) h2[t][ob] = mfma4(wq[k % 3][ob], h1[t][k >> 2][k & 3], h2[t][ob]);
-      if (DDRL_FWD_INTERLEAVE && (k >> 2) + 1 < 4)
-#pragma unroll
-        for (int t = 0; t < RT; ++t) h1[t][(k >> 2) + 1][k & 3] = tanh_fast(h1[t][(k >> 2) + 1][k & 3]);
       __builtin_amdgcn_sched_barrier(0);
     }
   }

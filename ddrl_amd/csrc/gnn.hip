@@ -131,8 +131,9 @@ __device__ __forceinline__ float quad_next(float v) { return dpp_mov<0x39>(v); }
 // the same for the reduction's and Adam's outputs measured no gain).
 // The one-launch step (l2: the partials are read by reducers on the same XCD in the same
 // launch, gnn_tail) keeps them in the XCD's L2 with plain stores instead.
+// (measured at C5, 2048 envs, one box: plain 18.19 us per step, nontemporal 18.58)
 #ifndef DDRL_GNN_L2_PLAIN
-#define DDRL_GNN_L2_PLAIN 0
+#define DDRL_GNN_L2_PLAIN 1
 #endif
 __device__ __forceinline__ void pst(bool l2, float* p, float v) {
   if (l2 && DDRL_GNN_L2_PLAIN) *p = v;
