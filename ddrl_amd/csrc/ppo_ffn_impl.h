@@ -602,6 +602,13 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 
   NetLds W;
   constexpr int LD = ROWS + 8;              // feature-major image stride
+  // K (rows) of the weight-gradient tiles; the timing-only cost-model build
+  // -DDDRL_ABL_HALF_DW halves it (the weight-gradient work of a four-way row split)
+#ifdef DDRL_ABL_HALF_DW
+  constexpr int DWR = ROWS / 2;
+#else
+  constexpr int DWR = ROWS;
+#endif
   float* bufA = lds + BRANCH_LDS_FLOATS;    // feature-major [64][LD]: H1, then X
   float* bufB = bufA + 64 * LD;             // feature-major [64][LD]: dZ2, then dZ1
   float* Pb = bufB + 64 * LD;               // [NW][NSB] per-wave partial small grads
@@ -891,12 +898,12 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     if constexpr (HMF) {
       static_assert(NW == 4, "one head tile (16 features) per wave");
       floatx4 gh;
-      dw_tiles_fm_head<ROWS, NS1>(bufA, bufB, tfa, w & 3, gt, bufH, bufD, w, gh);   // dW2 tiles + dWo
+      dw_tiles_fm_head<DWR, NS1, ROWS + 8>(bufA, bufB, tfa, w & 3, gt, bufH, bufD, w, gh);   // dW2 tiles + dWo
       if (c < OB)
 #pragma unroll
         for (int r = 0; r < 4; ++r) Pb[(16 * w + 4 * q + r) * OB + c] = gh[r];
     } else {
-      dw_tiles_fm<ROWS, NS1>(bufA, bufB, tfa, w & 3, gt);   // dW2 tiles of this wave
+      dw_tiles_fm<DWR, NS1, ROWS + 8>(bufA, bufB, tfa, w & 3, gt);   // dW2 tiles of this wave
     }
 #else
     for (int i = 0; i < NS1; ++i) gt[i] = splat4(0.f);
@@ -946,11 +953,11 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 #ifdef DDRL_ABL_NO_DW1
       n1 = -1;
 #endif
-      if (n1 == NS2) dw_tiles_fm<ROWS, NS2>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
+      if (n1 == NS2) dw_tiles_fm<DWR, NS2, ROWS + 8>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
       else if constexpr (NS2 >= 3) {
-        if (n1 == 2) dw_tiles_fm<ROWS, 2>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
-        else if (n1 == 1) dw_tiles_fm<ROWS, 1>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
-      } else if (n1 == 1) dw_tiles_fm<ROWS, 1>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
+        if (n1 == 2) dw_tiles_fm<DWR, 2, ROWS + 8>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
+        else if (n1 == 1) dw_tiles_fm<DWR, 1, ROWS + 8>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
+      } else if (n1 == 1) dw_tiles_fm<DWR, 1, ROWS + 8>(bufA, bufB, tfa + NS1, w & 3, gt + NS1);
     }
     STAMP(10);
     if constexpr (KSP == 2) {
@@ -971,6 +978,16 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       });
 #else
       gx_get<NP>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), gtag, o, ub.err, [] {});
+#endif
+#ifdef DDRL_ABL_XCHG3
+      // timing-only cost-model build: the two more partner reads of a four-way row split, one
+      // after the other (each a poll of the partner's outbox and the transfer of its partials)
+      for (int extra = 0; extra < 2; ++extra) {
+        float o2[2 * NP];
+        gx_get<NP>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), gtag, o2, ub.err, [] {});
+#pragma unroll
+        for (int k = 0; k < 2 * NP; ++k) o[k] += 0.f * o2[k];
+      }
 #endif
 #pragma unroll
       for (int k = 0; k < NSLOT; ++k) gs[k] += o[k];

@@ -39,35 +39,38 @@ def run(n, variants):
         print(f"{v or 'baseline':28s} {out.stdout.strip()} {out.stderr.strip()[-200:]}", flush=True)
 
 
-def one(lib, n):
+def one(lib, n, env="QuantrupedMultiEnv_Local"):
+    """us per sequential minibatch step of the fused update of `env` (Local: 4 policies, d = 35;
+    SharedDecentral: 1 policy over 4 leg agents, d = 19) at n envs, T = 200."""
     import numpy as np, torch
     from ddrl_amd import native as N
     N.load(lib)
     from ddrl_amd.spec import make_cfg
     from ddrl_amd.trainer import glorot_ffn_flat
     T = 200
-    cfg, _ = make_cfg("QuantrupedMultiEnv_Local", n, T)
+    cfg, _ = make_cfg(env, n, T)
+    P = cfg.n_policies
     ctx = N.Context(cfg, 0, torch.cuda.current_stream().cuda_stream)
     rng = np.random.default_rng(0)
-    for p in range(4):
-        ctx.params_set(p, glorot_ffn_flat(rng, 35, 2))
+    for p in range(P):
+        ctx.params_set(p, glorot_ffn_flat(rng, cfg.obs_dim[p], 2))
         lay = ctx.layout[p]
         r = rng.normal(size=(T * lay["C"], lay["stride"])).astype(np.float32) * 0.5
         ctx.records_set(p, r)
-    R = T * n
+    R = T * ctx.layout[0]["C"]
     nb = R // 128
-    sh = [torch.from_numpy(rng.permutation(R).astype(np.int32)).cuda() for _ in range(4)]
+    sh = [torch.from_numpy(rng.permutation(R).astype(np.int32)).cuda() for _ in range(P)]
     pe = [torch.from_numpy(np.stack([rng.permutation(nb) for _ in range(10)]).astype(np.int32)).cuda()
-          for _ in range(4)]
+          for _ in range(P)]
     best = 1e9
     for _ in range(3):
         t0 = time.perf_counter()
-        ctx.ppo_update(0xF, sh, pe, [0.2] * 4)
+        ctx.ppo_update((1 << P) - 1, sh, pe, [0.2] * P)
         ctx.synchronize()
         best = min(best, time.perf_counter() - t0)
     import hashlib
     h = hashlib.sha256()
-    for p in range(4):
+    for p in range(P):
         h.update(ctx.params_get(p).tobytes())
         for a in ctx.adam_get(p)[:2]:
             h.update(np.asarray(a).tobytes())
@@ -81,4 +84,4 @@ if __name__ == "__main__":
     elif sys.argv[1] == "run":
         run(int(sys.argv[2]) if len(sys.argv) > 2 else 512, sys.argv[3:] or VARIANTS)
     else:
-        one(sys.argv[2], int(sys.argv[3]))
+        one(sys.argv[2], int(sys.argv[3]), *sys.argv[4:5])
