@@ -24,6 +24,10 @@
 #else
 #define DDRL_XCHG_IS_ATOMIC 0
 #endif
+// LSB-tagged quads for fused launches (round 4; -DDDRL_LX=0: the {value, tag} pairs everywhere)
+#ifndef DDRL_LX
+#define DDRL_LX 1
+#endif
 
 namespace {
 
@@ -516,6 +520,57 @@ __device__ __forceinline__ bool gx_get(gx_box_t r, unsigned tag, float* out, int
 }
 #endif
 
+// Fused-update exchange with the tag in the values themselves (LX, round 4): four values per
+// 16-byte granule, each carrying a 1-bit step tag in its mantissa LSB, so the exchanged bytes
+// halve against {value, tag, value, tag}.  A value is valid exactly when its LSB is the step's
+// tag bit: every 4-byte value is its own single-copy-atomic unit, no 16-byte atomicity is
+// assumed.  The bit toggles between the two uses of an outbox (outboxes alternate by step
+// parity, the bit is (step >> 1) & 1, inverted), so a value from two steps back carries the other
+// bit; one from four steps back cannot reappear, because this lane read the location's
+// two-steps-back value and a location's value only moves forward.  The outboxes are cleared
+// before every fused launch (zero words fail the first two steps' bit 1).  Both workgroups of a
+// branch add the same two LSB-replaced partials, so their sums stay bit-identical; the
+// replaced bit is < 1 ulp of each partial.  Data-parallel gradient launches (one step per
+// launch) keep the epoch-tagged pairs, which need no clear per launch.
+__device__ __forceinline__ unsigned lx_bit(int step) { return ((unsigned)(step >> 1) & 1u) ^ 1u; }
+__device__ __forceinline__ float lx_t(float v, unsigned bit) { return __uint_as_float((__float_as_uint(v) & ~1u) | bit); }
+#if !DDRL_XCHG_IS_ATOMIC
+__device__ __forceinline__ void gx_put4(gx_box_t r, int j, float a, float b, float c, float d, unsigned bit) {
+  const v4u g = {__float_as_uint(lx_t(a, bit)), __float_as_uint(lx_t(b, bit)), __float_as_uint(lx_t(c, bit)),
+                 __float_as_uint(lx_t(d, bit))};
+  __builtin_amdgcn_raw_buffer_store_b128(g, r, (j * 256 + (int)threadIdx.x) * 16, 0, DDRL_GX_ST);
+}
+template <int NQ, typename F>
+__device__ __forceinline__ bool gx_get4(gx_box_t r, unsigned bit, float* out, int* err, F&& after_first) {
+  bool lost = false;
+  v4u g[NQ];
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  bool first = true;
+  for (;;) {
+    xchg_inv_l1();
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) g[j] = __builtin_amdgcn_raw_buffer_load_b128(r, (j * 256 + (int)threadIdx.x) * 16, 0, DDRL_GX_LD);
+    if (first) { after_first(); first = false; }
+    unsigned bad = 0;
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) bad |= (g[j][0] ^ bit) | (g[j][1] ^ bit) | (g[j][2] ^ bit) | (g[j][3] ^ bit);
+    if ((bad & 1u) == 0) break;
+    if (xchg_abandon(t0, err)) {
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) g[j] = v4u{0u, 0u, 0u, 0u};
+      lost = true;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+#pragma unroll
+  for (int j = 0; j < NQ; ++j)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) out[4 * j + k] = __uint_as_float(g[j][k]);
+  return lost;
+}
+#endif
+
 // dH2^T = Wo . dout^T on the matrix cores (policy head, O = 2A >= 4 outputs): one
 // 16x16x4 MFMA per feature block and 4 outputs, A = Wo[f = 16 fb + c][o = 4 kk + q] (LDS),
 // B = dout[row c][4 kk + q]; the result lands in the transposed activation layout
@@ -579,7 +634,7 @@ __device__ __forceinline__ void dw_tiles_fm_head(const float* A, const float* B,
   }
 }
 
-template <int A, int KS1, int OB, bool POL, int NW, int KSP, bool CUP>
+template <int A, int KS1, int OB, bool POL, int NW, int KSP, bool CUP, bool LSBX>
 __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBatch& ub, float* lds, int p, int kq) {
   constexpr int ROWS = DDRL_MB / KSP;
   constexpr int NT = Geo<NW, ROWS>::NT, RT = Geo<NW, ROWS>::RT, NS1 = Geo<NW, ROWS>::NS1, NS2 = Geo<NW, ROWS>::NS2;
@@ -599,6 +654,13 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   constexpr int NP0 = (NSLOT + 2) / 2;              // exchange pairs: small params + stats,
   constexpr int NP = NP0 + 2 * NTS;                  // then the owned dW tiles (KSP = 2)
   static_assert(KSP == 1 || (NT == 256 && NP == gx_pairs(OB, NW) && NP <= GX_MAX_PAIRS), "exchange pairs");
+  // fused launches (LSBX) sum LSB-replaced partials; the default protocol also exchanges them as
+  // LSB-tagged quads (LX: small params + stats, then one quad per owned dW tile), the atomic one
+  // keeps its {value, tag} pairs and replaces the bits before the sum -- the same sums
+  constexpr bool LX = LSBX && KSP == 2 && !DDRL_XCHG_IS_ATOMIC;
+  constexpr int NQ0 = (NSLOT + 1 + 3) / 4;
+  constexpr int NQ = NQ0 + NTS;
+  static_assert(!LX || NQ <= GX_MAX_PAIRS, "exchange quads");
 
   NetLds W;
   constexpr int LD = ROWS + 8;              // feature-major image stride
@@ -866,6 +928,8 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     __syncthreads();                                     // #1: H1, dZ2, partials visible
     STAMP(5);
     const unsigned gtag = xchg_tag(ub.epoch, step);
+    const unsigned lbit = lx_bit(step);
+    (void)lbit;
     const size_t gx_box = (size_t)GX_MAX_PAIRS * 256 * 2;   // granules per outbox
     const gx_box_t gx_mine = gx_rsrc(ub.gx + ((gx_branch + kq) * 2 + (step & 1)) * gx_box);
     float gs[NSLOT];
@@ -889,6 +953,16 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       if (tid < NSTAT)
         for (int i = 0; i < NW; ++i) st_own += red[i * 8 + tid];
       v0[NSLOT] = st_own;
+#if !DDRL_XCHG_IS_ATOMIC
+      if constexpr (LX) {
+        float w0[4 * NQ0];
+#pragma unroll
+        for (int k = 0; k < 4 * NQ0; ++k) w0[k] = k <= NSLOT ? v0[k] : 0.f;
+#pragma unroll
+        for (int j = 0; j < NQ0; ++j) gx_put4(gx_mine, j, w0[4 * j], w0[4 * j + 1], w0[4 * j + 2], w0[4 * j + 3], lbit);
+        return;
+      }
+#endif
 #pragma unroll
       for (int j = 0; j < NP0; ++j) gx_put(gx_mine, j, v0[2 * j], v0[2 * j + 1], gtag, coh);
     };
@@ -911,6 +985,12 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     if constexpr (KSP == 2) {
 #pragma unroll
       for (int i = 0; i < NS1; ++i) {
+#if !DDRL_XCHG_IS_ATOMIC
+        if constexpr (LX) {
+          gx_put4(gx_mine, NQ0 + i, gt[i][0], gt[i][1], gt[i][2], gt[i][3], lbit);
+          continue;
+        }
+#endif
         gx_put(gx_mine, NP0 + 2 * i, gt[i][0], gt[i][1], gtag, coh);
         gx_put(gx_mine, NP0 + 2 * i + 1, gt[i][2], gt[i][3], gtag, coh);
       }
@@ -965,9 +1045,40 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       // both workgroups hold the same bits)
 #pragma unroll
       for (int i = NS1; i < NTS; ++i) {
+#if !DDRL_XCHG_IS_ATOMIC
+        if constexpr (LX) {
+          gx_put4(gx_mine, NQ0 + i, gt[i][0], gt[i][1], gt[i][2], gt[i][3], lbit);
+          continue;
+        }
+#endif
         gx_put(gx_mine, NP0 + 2 * i, gt[i][0], gt[i][1], gtag, coh);
         gx_put(gx_mine, NP0 + 2 * i + 1, gt[i][2], gt[i][3], gtag, coh);
       }
+#if !DDRL_XCHG_IS_ATOMIC
+      if constexpr (LX) {
+        float o4[4 * NQ];
+        gx_get4<NQ>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), lbit, o4, ub.err, [&] {
+          if (step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, inv_cpr_l, idxb, stg, U.R, ub.lds_bytes);
+        });
+#ifdef DDRL_ABL_XCHG3
+        for (int extra = 0; extra < 2; ++extra) {   // the cost-model build, as below
+          float o2[4 * NQ];
+          gx_get4<NQ>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), lbit, o2, ub.err, [] {});
+#pragma unroll
+          for (int k = 0; k < 4 * NQ; ++k) o4[k] += 0.f * o2[k];
+        }
+#endif
+        // both workgroups add the same two LSB-replaced partials
+#pragma unroll
+        for (int k = 0; k < NSLOT; ++k) gs[k] = lx_t(gs[k], lbit) + o4[k];
+        if (tid < NSTAT) red[96 + tid] = lx_t(st_own, lbit) + o4[NSLOT];
+#pragma unroll
+        for (int i = 0; i < NTS; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) gt[i][r] = lx_t(gt[i][r], lbit) + o4[4 * (NQ0 + i) + r];
+      } else
+#endif
+      {
       float o[2 * NP];
 #ifndef DDRL_ABL_NO_PREFETCH
       // the next step's record gathers go out right behind the first poll's loads (which
@@ -989,13 +1100,24 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
         for (int k = 0; k < 2 * NP; ++k) o[k] += 0.f * o2[k];
       }
 #endif
+      if constexpr (LSBX) {   // the atomic protocol of a fused launch: the quads' sums
 #pragma unroll
-      for (int k = 0; k < NSLOT; ++k) gs[k] += o[k];
-      if (tid < NSTAT) red[96 + tid] = st_own + o[NSLOT];
+        for (int k = 0; k < NSLOT; ++k) gs[k] = lx_t(gs[k], lbit) + lx_t(o[k], lbit);
+        if (tid < NSTAT) red[96 + tid] = lx_t(st_own, lbit) + lx_t(o[NSLOT], lbit);
 #pragma unroll
-      for (int i = 0; i < NTS; ++i)
+        for (int i = 0; i < NTS; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) gt[i][r] += o[2 * NP0 + 4 * i + r];
+          for (int r = 0; r < 4; ++r) gt[i][r] = lx_t(gt[i][r], lbit) + lx_t(o[2 * NP0 + 4 * i + r], lbit);
+      } else {
+#pragma unroll
+        for (int k = 0; k < NSLOT; ++k) gs[k] += o[k];
+        if (tid < NSTAT) red[96 + tid] = st_own + o[NSLOT];
+#pragma unroll
+        for (int i = 0; i < NTS; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) gt[i][r] += o[2 * NP0 + 4 * i + r];
+      }
+      }
       STAMP(14);
     } else {
 #pragma unroll
@@ -1193,7 +1315,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   }
 }
 
-template <int A, int KS1, int KSP, bool CUP>
+template <int A, int KS1, int KSP, bool CUP, bool LSBX>
 __global__ void __launch_bounds__(64 * waves_for(A, KSP)) k_update_ffn(UpdateBatch ub) {
   extern __shared__ float lds[];
   constexpr int NW = waves_for(A, KSP);
@@ -1209,8 +1331,8 @@ __global__ void __launch_bounds__(64 * waves_for(A, KSP)) k_update_ffn(UpdateBat
   if (p >= ub.h.P) return;
   const int j = blockIdx.x >> 3, branch = j / KSP, kq = j - branch * KSP;
   const UpdateArgs U = ub.a[p];
-  if (branch) update_loop<A, KS1, 1, false, NW, KSP, false>(U, ub, lds, p, kq);
-  else update_loop<A, KS1, 2 * A, true, NW, KSP, CUP>(U, ub, lds, p, kq);
+  if (branch) update_loop<A, KS1, 1, false, NW, KSP, false, LSBX>(U, ub, lds, p, kq);
+  else update_loop<A, KS1, 2 * A, true, NW, KSP, CUP, LSBX>(U, ub, lds, p, kq);
 }
 
 // stride: the widest record stride of the launched policies (staging buffer rows)
@@ -1224,12 +1346,14 @@ static size_t update_lds_bytes(int O, int stride, int ksp) {
 }
 
 template <int A, int KS1, bool CUP = false>
-static void launch_update_t(hipStream_t s, UpdateBatch& ub, int P, int stride, int ksp) {
+static void launch_update_t(hipStream_t s, UpdateBatch& ub, int P, int stride, int ksp, bool lx) {
   ub.lds_bytes = (unsigned)update_lds_bytes(2 * A, stride, ksp);
-  if (ksp == 2)
-    hipLaunchKernelGGL((k_update_ffn<A, KS1, 2, CUP>), dim3(24 + P), dim3(64 * waves_for(A, 2)), ub.lds_bytes, s, ub);
+  if (ksp == 2 && lx)
+    hipLaunchKernelGGL((k_update_ffn<A, KS1, 2, CUP, true>), dim3(24 + P), dim3(64 * waves_for(A, 2)), ub.lds_bytes, s, ub);
+  else if (ksp == 2)
+    hipLaunchKernelGGL((k_update_ffn<A, KS1, 2, CUP, false>), dim3(24 + P), dim3(64 * waves_for(A, 2)), ub.lds_bytes, s, ub);
   else
-    hipLaunchKernelGGL((k_update_ffn<A, KS1, 1, CUP>), dim3(8 + P), dim3(64 * waves_for(A, 1)), ub.lds_bytes, s, ub);
+    hipLaunchKernelGGL((k_update_ffn<A, KS1, 1, CUP, false>), dim3(8 + P), dim3(64 * waves_for(A, 1)), ub.lds_bytes, s, ub);
 }
 
 }  // namespace
@@ -1251,12 +1375,13 @@ void DDRL_FFN_LAUNCH(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, 
   // of any granule left in the buffers, so a stale granule can never match.  (A memset per
   // launch costs a fill kernel and a boundary, ~5 us, per data-parallel step.)
   ub.epoch = (*epoch_ctr)++ % 4095u + 1u;
-  if (ub.epoch == 1) {
-    (void)hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * 8 * DDRL_MAXP, s);
-    (void)hipMemsetAsync(gx, 0, gx_bytes(DDRL_MAXP), s);
-  }
+  // fused launches (no gradient export) exchange LSB-tagged quads: their outboxes start cleared
+  // in every launch (one fill per iteration); gradient launches keep the epoch-tagged pairs
+  const bool lx = ksp == 2 && ua[0].grad_out == nullptr && DDRL_LX;
+  if (ub.epoch == 1) (void)hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * 8 * DDRL_MAXP, s);
+  if (ub.epoch == 1 || (lx && !DDRL_XCHG_IS_ATOMIC)) (void)hipMemsetAsync(gx, 0, gx_bytes(DDRL_MAXP), s);
   if (cup)   // "cup": one shared leg policy, A = 2, d <= 20 (capi validate)
-    launch_update_t<2, 5, true>(s, ub, h.P, stride, ksp);
+    launch_update_t<2, 5, true>(s, ub, h.P, stride, ksp, lx);
   else
-    DDRL_DISPATCH_A_KS1(A, d, launch_update_t, s, ub, h.P, stride, ksp);
+    DDRL_DISPATCH_A_KS1(A, d, launch_update_t, s, ub, h.P, stride, ksp, lx);
 }
