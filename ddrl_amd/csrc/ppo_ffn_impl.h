@@ -540,16 +540,21 @@ __device__ __forceinline__ void gx_put4(gx_box_t r, int j, float a, float b, flo
                  __float_as_uint(lx_t(d, bit))};
   __builtin_amdgcn_raw_buffer_store_b128(g, r, (j * 256 + (int)threadIdx.x) * 16, 0, DDRL_GX_ST);
 }
-template <int NQ, typename F>
-__device__ __forceinline__ bool gx_get4(gx_box_t r, unsigned bit, float* out, int* err, F&& after_first) {
+// NX > 0: the timing-only cost-model build of a four-way split; NX more quads (another outbox,
+// rx) loaded with every poll and returned unchecked
+template <int NQ, int NX = 0, typename F>
+__device__ __forceinline__ bool gx_get4(gx_box_t r, unsigned bit, float* out, int* err, F&& after_first,
+                                        gx_box_t rx = gx_box_t()) {
   bool lost = false;
-  v4u g[NQ];
+  v4u g[NQ + NX];
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   bool first = true;
   for (;;) {
     xchg_inv_l1();
 #pragma unroll
     for (int j = 0; j < NQ; ++j) g[j] = __builtin_amdgcn_raw_buffer_load_b128(r, (j * 256 + (int)threadIdx.x) * 16, 0, DDRL_GX_LD);
+#pragma unroll
+    for (int j = 0; j < NX; ++j) g[NQ + j] = __builtin_amdgcn_raw_buffer_load_b128(rx, (j * 256 + (int)threadIdx.x) * 16, 0, DDRL_GX_LD);
     if (first) { after_first(); first = false; }
     unsigned bad = 0;
 #pragma unroll
@@ -557,14 +562,14 @@ __device__ __forceinline__ bool gx_get4(gx_box_t r, unsigned bit, float* out, in
     if ((bad & 1u) == 0) break;
     if (xchg_abandon(t0, err)) {
 #pragma unroll
-      for (int j = 0; j < NQ; ++j) g[j] = v4u{0u, 0u, 0u, 0u};
+      for (int j = 0; j < NQ + NX; ++j) g[j] = v4u{0u, 0u, 0u, 0u};
       lost = true;
       break;
     }
     __builtin_amdgcn_s_sleep(1);
   }
 #pragma unroll
-  for (int j = 0; j < NQ; ++j)
+  for (int j = 0; j < NQ + NX; ++j)
 #pragma unroll
     for (int k = 0; k < 4; ++k) out[4 * j + k] = __uint_as_float(g[j][k]);
   return lost;
@@ -1056,11 +1061,23 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       }
 #if !DDRL_XCHG_IS_ATOMIC
       if constexpr (LX) {
+#ifdef DDRL_ABL_XCHG3P
+        // timing-only cost-model build: three partners' outboxes polled at once, every load of
+        // the three in flight together, and their sum (here the partner's outbox, checked, and
+        // 2 NQ quads of its other-parity outbox, unchecked)
+        float o4[12 * NQ];
+        gx_get4<NQ, 2 * NQ>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), lbit, o4, ub.err, [&] {
+          if (step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, inv_cpr_l, idxb, stg, U.R, ub.lds_bytes);
+        }, gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + ((step + 1) & 1)) * gx_box));
+#pragma unroll
+        for (int k = 0; k < 4 * NQ; ++k) o4[k] = (o4[k] + o4[4 * NQ + k]) + o4[8 * NQ + k];
+#else
         float o4[4 * NQ];
         gx_get4<NQ>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), lbit, o4, ub.err, [&] {
           if (step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, inv_cpr_l, idxb, stg, U.R, ub.lds_bytes);
         });
-#ifdef DDRL_ABL_XCHG3
+#endif
+#if defined(DDRL_ABL_XCHG3)
         for (int extra = 0; extra < 2; ++extra) {   // the cost-model build, as below
           float o2[4 * NQ];
           gx_get4<NQ>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), lbit, o2, ub.err, [] {});
