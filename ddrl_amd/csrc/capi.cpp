@@ -90,6 +90,11 @@ struct ddrl_ctx {
   // host-variant staging
   float *h_obs = nullptr, *h_eps = nullptr, *h_act = nullptr;
   ncclComm_t comm = nullptr;           // data-parallel learner (ddrl_comm_init)
+  float* ddp_chunk = nullptr;          // ddrl_ppo_update_ddp: pre-gathered records of a run of steps
+  size_t ddp_chunk_n = 0;
+  int32_t* ddp_slots = nullptr;        // ... and the minibatch slot of every step (device copy)
+  size_t ddp_slots_n = 0;
+  std::vector<int32_t> ddp_slots_host; // source of that copy, alive until the call's final sync
   float *h_fw = nullptr, *h_cfrc = nullptr;
   uint8_t* h_done = nullptr;
   // ddrl_rollout_fragment as one HIP graph (T x (act, reward, filter push, observe) +
@@ -1021,15 +1026,40 @@ int ddrl_ppo_update_ddp(ddrl_ctx* c, int pid, const int32_t* shuffle, const int3
       ua[(size_t)e * nb + b] = u;
     }
   const bool ffn = c->cfg.model_kind == DDRL_MODEL_FFN;
+  // the records of each run of up to DDP_CHUNK_STEPS steps are gathered into one contiguous
+  // chunk first (stream order: after the previous run's last gradient launch), so a one-step
+  // gradient launch stages its rows without the dependent perm -> shuffle index loads
+  constexpr int DDP_CHUNK_STEPS = 1024;
+  const int CH = std::min(DDP_CHUNK_STEPS, steps);
+  const int stride = P.lay.stride;
+  const size_t need = (size_t)CH * m * stride;
+  if (c->ddp_chunk_n < need) {
+    if (dalloc(c, &c->ddp_chunk, need)) return -1;
+    c->ddp_chunk_n = need;
+  }
+  if (c->ddp_slots_n < (size_t)steps) {
+    if (dalloc(c, &c->ddp_slots, (size_t)steps)) return -1;
+    c->ddp_slots_n = (size_t)steps;
+  }
+  c->ddp_slots_host.assign(perm, perm + steps);
+  HIPCHK(hipMemcpyAsync(c->ddp_slots, c->ddp_slots_host.data(), sizeof(int32_t) * steps, hipMemcpyHostToDevice,
+                        c->stream));
   c->kl_last[pid] = kl;
   if (ffn && snapshot(c, 1 << pid)) return -1;   // restored by check_err if any step fails
   for (int s = 0; s < steps; ++s) {
+    const int k = s % CH;
+    if (k == 0) launch_rows_gather(c->stream, P.rec, stride, shuffle, c->ddp_slots, m, s, std::min(CH, steps - s),
+                                   c->ddp_chunk);
+    float* rows = c->ddp_chunk + (size_t)k * m * stride;
     // test hook: step s's gradient is lost (its Adam launch and every later one skip)
     if (s == c->fail_step) HIPCHK(hipMemsetD32Async((hipDeviceptr_t)c->err, 1, 1, c->stream));
-    if (ffn)
-      launch_ffn(c, &ua[s], h, m, inv_n, P.d, P.lay.stride, grad_split(c, m), 1);
-    else
-      launch_step_gnn(c->stream, ua[s], h, 0, m, inv_n, c->gnn, nullptr, c->cfg.gnn_layer);
+    if (ffn) {
+      ua[s].rec = rows;
+      ua[s].shuffle = nullptr;   // rows 0 .. m of the slice
+      launch_ffn(c, &ua[s], h, m, inv_n, P.d, stride, grad_split(c, m), 1);
+    } else {
+      launch_step_gnn(c->stream, ua[s], h, 0, m, inv_n, c->gnn, rows, c->cfg.gnn_layer);
+    }
     NCCLCHK(ncclAllReduce(P.grad, P.grad, (size_t)P.n_params, ncclFloat32, ncclSum, c->comm, c->stream));
     launch_apply_adam(c->stream, P.grad, P.n_params, P.theta, P.m, P.v, P.beta_pow, h, gscale, pid, c->err);
   }

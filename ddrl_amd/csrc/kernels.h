@@ -120,7 +120,7 @@ void launch_gae(hipStream_t s, const GaeBatch& gb);   // every policy of the con
 struct UpdateArgs {
   const float* rec; RecLayout lay;
   int d, A, R;                 // obs width, action dim, rows of this policy
-  const int32_t* shuffle;      // [R]
+  const int32_t* shuffle;      // [R]; null: the minibatch rows are rec[0 .. rows) (pre-gathered)
   const int32_t* perm;         // [E][nb]
   int nb, n_epochs, max_steps, step0;
   float* theta; float* m; float* v; float* beta_pow;   // beta_pow[2]
@@ -217,3 +217,6 @@ void launch_step_gnn(hipStream_t s, const UpdateArgs& u, const UpdateHyper& h, i
 // the records of minibatch steps [step0, step0 + n_steps) of the schedule -> dst
 // ([n_steps][128][stride], n_steps <= GNN_CHUNK_STEPS): one bandwidth-bound gather per chunk
 void launch_gnn_gather(hipStream_t s, const UpdateArgs& u, int step0, int n_steps, float* dst);
+// data-parallel steps: step k's m minibatch rows gathered into dst[k][m][stride] (ppo_ffn.hip)
+void launch_rows_gather(hipStream_t s, const float* rec, int stride, const int32_t* shuffle, const int32_t* perm,
+                        int m, int step0, int n_steps, float* dst);

@@ -140,3 +140,25 @@ void launch_apply_adam(hipStream_t s, const float* grad, int n, float* theta, fl
   else
     hipLaunchKernelGGL(k_apply_adam<0>, dim3(1), dim3(1024), 0, s, grad, n, theta, m, v, beta_pow, h, gscale, 0, err);
 }
+
+// Pre-gather of a run of data-parallel steps (ddrl_ppo_update_ddp): step k's m rows,
+// dst[k][i][col] = rec[shuffle[perm[step0 + k] * m + i] * stride + col], so every one-step
+// gradient launch stages its records from one contiguous slice instead of through the two
+// dependent index loads (perm, then shuffle) ahead of its record gathers.  One float per thread.
+__global__ void k_rows_gather(const float* __restrict__ rec, int stride, const int32_t* __restrict__ shuffle,
+                              const int32_t* __restrict__ perm, int m, int step0, size_t n, float* __restrict__ dst) {
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= n) return;
+  const size_t rowg = gid / stride;
+  const int col = (int)(gid - rowg * stride);
+  const int k = (int)(rowg / m), i = (int)(rowg - (size_t)k * m);
+  const int row = shuffle[(size_t)perm[step0 + k] * m + i];
+  dst[gid] = rec[(size_t)row * stride + col];
+}
+
+void launch_rows_gather(hipStream_t s, const float* rec, int stride, const int32_t* shuffle, const int32_t* perm,
+                        int m, int step0, int n_steps, float* dst) {
+  const size_t n = (size_t)n_steps * m * stride;
+  hipLaunchKernelGGL(k_rows_gather, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, rec, stride, shuffle, perm, m,
+                     step0, n, dst);
+}

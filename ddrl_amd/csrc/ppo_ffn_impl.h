@@ -329,6 +329,7 @@ __device__ __forceinline__ void write_stats(float* so, const float* red, float i
 
 __device__ __forceinline__ int row_index(const UpdateArgs& U, int step, int row_l, bool ok) {
   if (!ok) return 0;
+  if (!U.shuffle) return row_l;   // pre-gathered rows (data-parallel one-step launches)
   const int e = step / U.nb, b = step - e * U.nb;
 #ifdef DDRL_BOUNDS
   if (!BCHK(e >= 0 && e < U.n_epochs, 2)) return 0;
