@@ -351,8 +351,11 @@ __device__ __forceinline__ int perm_slot(const UpdateArgs& U, int step) {
 #ifdef DDRL_STAMPS
 __device__ unsigned long long g_stamps[32][16];
 #define STAMP_INIT unsigned long long st_prev = __builtin_amdgcn_s_memtime(), st_acc[16] = {0};
-#define STAMP(k) do { if (tid == 0) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[k] += t_ - st_prev; st_prev = t_; } } while (0)
-#define STAMP_DONE do { if (tid == 0) for (int k_ = 0; k_ < 16; ++k_) g_stamps[blockIdx.x][k_] = st_acc[k_]; } while (0)
+#ifndef DDRL_STAMP_TID   // the stamped thread (lane 0 of a wave): per-wave diagnostic builds
+#define DDRL_STAMP_TID 0
+#endif
+#define STAMP(k) do { if (tid == DDRL_STAMP_TID) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[k] += t_ - st_prev; st_prev = t_; } } while (0)
+#define STAMP_DONE do { if (tid == DDRL_STAMP_TID) for (int k_ = 0; k_ < 16; ++k_) g_stamps[blockIdx.x][k_] = st_acc[k_]; } while (0)
 }  // namespace
 #if !DDRL_FFN_AT
 extern "C" int ddrl_diag_stamps(unsigned long long* host) {
