@@ -120,6 +120,31 @@ def test_atomic_exchange_matches_default_protocol_bit_for_bit():
     np.testing.assert_array_equal(st_a, st_b)
 
 
+def test_short_launches_match_atomic_protocol_bit_for_bit():
+    """Consecutive fused launches of 1, 2, 3 and 5 steps: every launch clears the outboxes and
+    restarts the one-bit LSB tags at step 0, so the first steps of each launch (zero words
+    must fail the tag) and a tag's return after two steps are exercised launch after launch.
+    The atomic protocol sums the same LSB-replaced partials through {value, tag} pairs."""
+    P = 4
+    res = []
+    for env in ({}, {"DDRL_XCHG": "atomic"}):
+        ctx, cfg, inst = _ctx(**env)
+        _prepare(ctx, cfg, inst)
+        st = []
+        for i, k in enumerate((1, 2, 3, 5)):
+            sh, pe = _schedule(ctx, P, seed=100 + i)
+            ctx.ppo_update((1 << P) - 1, sh, pe, [0.2] * P, max_steps=k)
+            st.append(ctx.ppo_stats(0, k))
+        res.append((_state(ctx, P), st))
+        ctx.close()
+    (sa, st_a), (sb, st_b) = res
+    for x, y in zip(sa, sb):
+        for u, v in zip(x, y):
+            np.testing.assert_array_equal(np.asarray(u), np.asarray(v))
+    for a, b in zip(st_a, st_b):
+        np.testing.assert_array_equal(a, b)
+
+
 @pytest.fixture()
 def pg1():
     import torch.distributed as dist
