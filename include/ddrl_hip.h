@@ -255,7 +255,10 @@ int ddrl_comm_allreduce(ddrl_ctx* ctx, float* buf_dev, size_t n);
  * loop of ddrl_amd/ddp.py DataParallelLearner.learn without a host round trip per call.
  *   shuffle_dev: this rank's row permutation; perm_host[n_epochs][nb]: minibatch slots;
  *   rows_per_rank: 128 / ranks ("split") or 128 ("local"); grad_scale: 1 or 1 / ranks.
- * Learner statistics of the last epoch land in ddrl_ppo_stats rows 0 .. nb - 1. */
+ * Learner statistics of the last epoch land in ddrl_ppo_stats rows 0 .. nb - 1.
+ * The records of each run of up to 1,024 steps are gathered on the device into one chunk
+ * (allocated by the first call: min(1024, steps) x rows_per_rank x record stride floats) before
+ * that run's gradient launches; perm_host is copied to the device once per call. */
 int ddrl_ppo_update_ddp(ddrl_ctx* ctx, int pid, const int32_t* shuffle_dev, const int32_t* perm_host,
                         int n_epochs, int nb, int rows_per_rank, float kl_coeff, float grad_scale);
 
