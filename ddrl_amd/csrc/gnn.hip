@@ -1045,11 +1045,10 @@ __device__ __forceinline__ void gnn_tail(const GnnArgs& ga, float* lds, int tile
   const bool ok = tid >= ga.ntiles || gnn_wait_flag(ga, ga.flags + 8 * tid + k, t0);
   if (!__syncthreads_and(ok)) return;
   if (stats) {
-    if (tid < 5) {   // all 32 loads in flight, then summed in tile order
+    if (tid < 5) {   // all 32 loads in flight (all 32 tiles on this path), then summed in tile order
       float sv[DDRL_MB / 4];
 #pragma unroll
-      for (int t = 0; t < DDRL_MB / 4; ++t)
-        sv[t] = t < ga.ntiles ? sc1_ld(ga.statp + (net * (DDRL_MB / 4) + t) * 8 + tid) : 0.f;
+      for (int t = 0; t < DDRL_MB / 4; ++t) sv[t] = sc1_ld(ga.statp + (net * (DDRL_MB / 4) + t) * 8 + tid);
       float a = 0.f;
 #pragma unroll
       for (int t = 0; t < DDRL_MB / 4; ++t) a += sv[t];
@@ -1072,14 +1071,18 @@ __device__ __forceinline__ void gnn_tail(const GnnArgs& ga, float* lds, int tile
   }
   RSTAMPB(ga.rbase[k] + r, 0);
   SPAN(1, ga.rbase[k] + r, 0);
-  // the reduction: 32 partials of this thread's parameter, in tile order
+  // the reduction: 32 partials of this thread's parameter (this path runs only with all 32
+  // tiles), in tile order.  The loads are unconditional -- a lane without a parameter reads
+  // parameter 0's and drops the sum -- so all 32 go out back to back: under a per-load
+  // condition the compiler branched around each one and waited for the first before the rest
   float v[DDRL_MB / 4];
+  const float* pp = ga.part + (pv ? p : 0);
 #pragma unroll
-  for (int t = 0; t < DDRL_MB / 4; ++t)
-    v[t] = (pv && t < ga.ntiles) ? sc1_ld(ga.part + (size_t)t * ga.part_stride + p) : 0.f;
+  for (int t = 0; t < DDRL_MB / 4; ++t) v[t] = sc1_ld(pp + (size_t)t * ga.part_stride);
   float g0 = 0.f;
 #pragma unroll
   for (int t = 0; t < DDRL_MB / 4; ++t) g0 += v[t];
+  if (!pv) g0 = 0.f;
   if (!adam) {   // data-parallel gradient: the all-reduce and Adam follow as launches
     if (pv) ga.grad[p] = g0;
     return;
