@@ -216,14 +216,18 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds, const in
       ridx = gvalid ? U.shuffle[U.perm[e * U.nb + b] * DDRL_MB + graph] : 0;
       X = U.rec + (size_t)ridx * U.lay.stride + U.lay.obs;
     }
-    sel = gvalid ? (int)X[92] : 0;
+    // unconditional load (X is a valid row for every lane), converted where it is used: a
+    // conditional one was waited for before any other record or weight load went out
+    const float selv = X[92];
+    sel = gvalid ? (int)selv : 0;
   }
   const float* xr = X + n * 23;
   float fi[GNI];
 #pragma unroll
   for (int k = 0; k < GNI; ++k) {
     const int i = w + 4 * k;
-    fi[k] = i < GF ? xr[i] : 0.f;
+    const float xv = xr[i < GF ? i : 0];
+    fi[k] = i < GF ? xv : 0.f;
   }
   const float qv = xr[GF + q];   // B operand of the hypernet MFMA: q_row[c][q]
 
