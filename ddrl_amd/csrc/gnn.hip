@@ -202,6 +202,11 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds, const in
   const float* X;
   int sel = 0;
   int ridx = 0;
+  constexpr int NPRE = NET ? 2 : 3 * A + 2;
+  float pre[NPRE];
+#pragma unroll
+  for (int j = 0; j < NPRE; ++j) pre[j] = 0.f;
+  float adv_m = 0.f, adv_d = 1.f;
   if constexpr (MODE == GNN_ACT) {
     X = ga.x + (size_t)(ga.act_e0 + (gvalid ? graph : 0)) * 92;
   } else if constexpr (MODE == GNN_FWD) {
@@ -220,6 +225,25 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds, const in
     // conditional one was waited for before any other record or weight load went out
     const float selv = X[92];
     sel = gvalid ? (int)selv : 0;
+    // the loss head's record fields (lanes 0-15: node c of graph c / 4), loaded here with the
+    // rest of the record: at the head, after the forward, they were one more memory latency on
+    // every step's path (an invalid graph reads graph 0's row; the loss masks it)
+    if (tid < 16) {
+      const float* rp = X - U.lay.obs;
+      if constexpr (NET == 0) {
+#pragma unroll
+        for (int j = 0; j < A; ++j) pre[j] = rp[U.lay.act + j];
+#pragma unroll
+        for (int j = 0; j < 2 * A; ++j) pre[A + j] = rp[U.lay.logit + j];
+        pre[3 * A] = rp[U.lay.logp];
+        pre[3 * A + 1] = rp[U.lay.adv];
+      } else {
+        pre[0] = rp[U.lay.vf];
+        pre[1] = rp[U.lay.vt];
+      }
+    }
+    adv_m = U.adv_norm[0];
+    adv_d = U.adv_norm[1];
   }
   const float* xr = X + n * 23;
   float fi[GNI];
@@ -482,20 +506,18 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds, const in
       for (int o = 0; o < O; ++o)
         out[o] = (((hp[cc * 4 + o] + hp[(16 + cc) * 4 + o]) + hp[(32 + cc) * 4 + o]) +
                   hp[(48 + cc) * 4 + o]) + th[off.bout + o];
-      const float* rp = ga.stage ? ga.stage + (size_t)(4 * tile + gg) * U.lay.stride
-                                 : U.rec + (size_t)ridx * U.lay.stride;
       if constexpr (NET == 0) {
         float act[A], ol[2 * A];
 #pragma unroll
-        for (int j = 0; j < A; ++j) act[j] = rp[U.lay.act + j];
+        for (int j = 0; j < A; ++j) act[j] = pre[j];
 #pragma unroll
-        for (int j = 0; j < 2 * A; ++j) ol[j] = rp[U.lay.logit + j];
-        const float adv = (rp[U.lay.adv] - U.adv_norm[0]) / U.adv_norm[1];
-        policy_loss_row<A>(out, act, ol, rp[U.lay.logp], adv, U.kl_coeff, 1.f - H.clip, 1.f + H.clip,
+        for (int j = 0; j < 2 * A; ++j) ol[j] = pre[A + j];
+        const float adv = (pre[3 * A + 1] - adv_m) / adv_d;
+        policy_loss_row<A>(out, act, ol, pre[3 * A], adv, U.kl_coeff, 1.f - H.clip, 1.f + H.clip,
                            H.ent_coeff, ga.inv_n, ok, dout, st);
         st[3] = st[4] = 0.f;
       } else {
-        value_loss_row(out[0], rp[U.lay.vf], rp[U.lay.vt], H, ga.inv_n, ok, dout, st);
+        value_loss_row(out[0], pre[0], pre[1], H, ga.inv_n, ok, dout, st);
       }
 #pragma unroll
       for (int o = 0; o < O; ++o) dsh[gg * 4 + o] = dout[o];
@@ -709,11 +731,10 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds, const in
   //   [dWenc | dbenc] (block j, qd) = sum over the 16 rows of dpre[row][j] [q_row | 1][qd]
   // as 4 MFMAs per block: dpre goes through a per-wave LDS tile to put rows on the k axis,
   // B = the rows' quaternions with a ones column (bias) at qd = 4.
+  // (wave 0's lane (c, q) holds component q of node c's quaternion since the start: qv; a
+  // reload from the record here put one memory latency before this barrier on every step)
   float* qt = lds + L_QT;
-  if (w == 0 && q == 0) {
-#pragma unroll
-    for (int d = 0; d < 4; ++d) qt[c * 4 + d] = xr[GF + d];
-  }
+  if (w == 0) qt[c * 4 + q] = qv;
   __syncthreads();
   float qb[4];
 #pragma unroll
