@@ -38,43 +38,51 @@ def metric_name(envs):
     return f"env-steps/sec at {envs} envs × 4 leg agents; PPO update ms/minibatch"
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense FP32 (MFMA f32 = vector rate), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
-PMC_SUMMARIES = [os.path.join(ROOT, "profiles", r, "pmc_summary.json") for r in ("r04", "r03")]
+PMC_SUMMARIES = [os.path.join(ROOT, "profiles", r, "pmc_summary.json") for r in ("r05", "r04", "r03")]
 PMC_WORKLOAD = {"QuantrupedMultiEnv_Local": "local", "QuantrupedMultiEnv_SharedDecentral": "c4",
                 "QuantrupedMultiEnv_DecentralShared_Graph": "c5"}
 
 
-def pmc_summary():
-    """The newest committed rocprofv3 PMC summary (tools/pmc_summary.py) and its path."""
+def pmc_key(env, gnn_tail=True):
+    """Workload key of the committed PMC passes; the three-launch GNN step has its own pass."""
+    k = PMC_WORKLOAD.get(env, "")
+    return k + "_3launch" if k == "c5" and not gnn_tail else k
+
+
+def pmc_summary(key=None):
+    """The newest committed rocprofv3 PMC summary (tools/pmc_summary.py) that holds `key` (any,
+    when None), and its path."""
     for path in PMC_SUMMARIES:
         try:
             with open(path) as f:
-                return json.load(f), os.path.relpath(path, ROOT)
+                s = json.load(f)
         except OSError:
             continue
+        if key is None or key in s.get("workloads", {}):
+            return s, os.path.relpath(path, ROOT)
     return None, None
 
 
-def pmc_workload(env):
-    s, path = pmc_summary()
-    w = (s or {}).get("workloads", {}).get(PMC_WORKLOAD.get(env, ""))
-    return w, path
+def pmc_workload(key):
+    s, path = pmc_summary(key)
+    return (s or {}).get("workloads", {}).get(key), path
 
 
-def pmc_traffic(env, policy_steps):
+def pmc_traffic(key, policy_steps):
     """HBM bytes of the update (all its launches) from the committed rocprofv3 PMC passes
-    (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE; tools/profile_r04.sh): the
+    (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE; tools/profile_r05.sh): the
     workload's bytes per (policy, minibatch) step times this update's steps -- the kernels'
     traffic is per step.  The counters cannot be read live from inside the timed run; None
     for a workload without a committed pass."""
-    w, _ = pmc_workload(env)
+    w, _ = pmc_workload(key)
     return w["hbm_bytes_per_step"] * policy_steps if w else None
 
 
-def pmc_mfma(env):
+def pmc_mfma(key):
     """MFMA-busy and effective clock of the workload's dominant update kernel from the committed
     counter pass (SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE with --kernel-trace; see
     tools/pmc_summary.py for the arithmetic), or {} without one."""
-    w, path = pmc_workload(env)
+    w, path = pmc_workload(key)
     m = (w or {}).get("mfma")
     if not m:
         return {}
@@ -104,130 +112,142 @@ def gnn_flops_per_row(A, H=64, F=19):
     return 3 * fwd + 2 * 4 * 4 * F * H * 2
 
 
+def _cpu_model(O, cfg, p):
+    """The oracle's model of policy p: (kind, params, shapes), Glorot-initialized from a seed
+    fixed per policy (the same in every worker of the parallel baseline)."""
+    rng, A = np.random.default_rng(1000 + p), cfg.act_dim
+    if cfg.model_kind == 1:   # "gnn" (DecentralShared_Graph): one shared GraphNet leg policy
+        return "gnn", O.gnn_init(rng, 2 * A), O.gnn_param_shapes(2 * A)
+    return "ffn", O.ffn_init(rng, cfg.obs_dim[p], 2 * A), O.ffn_param_shapes(cfg.obs_dim[p], 2 * A)
+
+
+def _cpu_rollout(O, cfg, inst, n_envs, T, rng):
+    """The oracle's rollout of one fragment over n_envs envs with its own env-side MeanStdFilter
+    (as every RLlib rollout worker process has): per step filter + routing, each policy's
+    forward over its rows (row c = env * k + slot for the policy's k agents), DiagGaussian
+    sampling, per-leg rewards; then the bootstrap and GAE per policy.  Returns the unstandardized
+    train batch of every policy."""
+    P, A = cfg.n_policies, cfg.act_dim
+    agents = list(inst.agent_names)
+    slots = [[a for j, a in enumerate(agents) if cfg.agent_policy[j] == p] for p in range(P)]
+    models = [_cpu_model(O, cfg, p) for p in range(P)]
+    obs = rng.normal(size=(T + 1, n_envs, cfg.obs_full_dim)).astype(np.float32)
+    eps = rng.normal(size=(T, n_envs, cfg.n_agents, A)).astype(np.float32)
+    fw = rng.normal(size=(T, n_envs)).astype(np.float32)
+    cfrc = rng.normal(size=(T, n_envs, 14, 6)).astype(np.float32)
+    rs = O.RunningStat((cfg.obs_full_dim,))
+    node_tables = [inst.obs_indices[a] for a in agents]
+
+    def forward(p, t_obs, z):
+        kind, params, _ = models[p]
+        if kind == "gnn":   # X [4][23] per env, one training row per node (c = env * 4 + node)
+            X = np.stack([O.graph_observation(t_obs[e].astype(np.float64), z[e], node_tables)
+                          for e in range(n_envs)]).astype(np.float32)
+            x, node = np.repeat(X, 4, axis=0), np.tile(np.arange(4), n_envs)
+            logits, value, _ = O.gnn_forward(params, x, node)
+            return (x, node), logits, value
+        x = np.stack([z[:, inst.obs_indices[a]] for a in slots[p]], 1).reshape(-1, cfg.obs_dim[p]).astype(np.float32)
+        logits, value, _ = O.ffn_forward(params, x)
+        return (x, None), logits, value
+
+    rec = [dict(obs=[], node=[], act=[], logits=[], logp=[], vf=[], rew=[]) for _ in range(P)]
+    tables = {a: inst.contact_force_indices[a] for a in agents}
+    z = O.mean_std_filter(obs[0], rs, True, 10.0)
+    for t in range(T):
+        actions = np.zeros((n_envs, 8))
+        for p in range(P):
+            (x, node), logits, value = forward(p, obs[t], z)
+            ep = eps[t][:, [agents.index(a) for a in slots[p]]].reshape(-1, A)
+            act = O.dg_sample(logits, ep)
+            for k, v in (("obs", x), ("node", node), ("act", act), ("logits", logits),
+                         ("logp", O.dg_logp(logits, act)), ("vf", value)):
+                rec[p][k].append(v)
+            for s, a in enumerate(slots[p]):
+                actions[:, inst.action_indices[a]] = np.clip(act.reshape(n_envs, len(slots[p]), A)[:, s], -1, 1)
+        rw = [O.per_leg_reward(float(fw[t, e]), cfrc[t, e], {a: actions[e, inst.action_indices[a]] for a in agents},
+                               tables, 0.5, 0.05) for e in range(n_envs)]
+        for p in range(P):
+            rec[p]["rew"].append(np.array([[rw[e][a] for a in slots[p]] for e in range(n_envs)],
+                                          np.float32).reshape(-1))
+        z = O.mean_std_filter(obs[t + 1], rs, True, 10.0)
+    out = []
+    for p in range(P):
+        r = rec[p]
+        last_v = forward(p, obs[T], z)[2]
+        vf, rew = np.stack(r["vf"]), np.stack(r["rew"])
+        adv, vt = O.gae_fragment(rew, vf, np.zeros(rew.shape, bool), last_v)
+        b = dict(actions=np.concatenate(r["act"]), logits=np.concatenate(r["logits"]),
+                 logp=np.concatenate(r["logp"]), vf_preds=vf.reshape(-1), adv=adv.reshape(-1), vt=vt.reshape(-1))
+        if models[p][0] == "gnn":
+            b.update(X=np.concatenate(r["obs"]), node_idx=np.concatenate(r["node"]))
+        else:
+            b.update(obs=np.concatenate(r["obs"]))
+        out.append(b)
+    return out
+
+
+def _cpu_update(O, cfg, p, batch, rng):
+    """One policy's minibatch SGD chain over its batch (10 epochs; sequential by construction:
+    every step needs the previous step's weights)."""
+    kind, params, shapes = _cpu_model(O, cfg, p)
+    adv, _, _ = O.standardize(batch["adv"])
+    sh, pe = O.sgd_schedule(rng, len(adv), 128, cfg.num_sgd_iter)
+    adam = O.Adam(sum(int(np.prod(s)) for _, s in shapes))
+    O.ppo_update(kind, params, shapes, adam, dict(batch, adv=adv), sh, pe, np.float32(0.2), {})
+
+
+def cpu_sample_envs(env, cpu_envs):
+    """Envs of the bounded CPU sample: cpu_envs for one agent per policy, divided by the agents
+    a shared policy trains on (the same rows per iteration), and by 16 for the GraphNet, whose
+    numpy step costs ~20x the fcnet's (about 10-30 s of CPU work either way)."""
+    from ddrl_amd.spec import make_cfg
+    cfg, _ = make_cfg(env, 1, 1)
+    k = max(sum(1 for j in range(cfg.n_agents) if cfg.agent_policy[j] == p) for p in range(cfg.n_policies))
+    return max(4, cpu_envs // (16 if cfg.model_kind == 1 else k))
+
+
 def cpu_baseline(env, n_envs=128, T=200, seed=0, threads=1):
-    """The numpy oracle on a bounded sample of the same workload (same env, same PPO
+    """The numpy oracle on a bounded sample of the same workload (same env and model, same PPO
     schedule, fewer envs), BLAS limited to `threads` threads.  Returns env-steps/s."""
     from threadpoolctl import threadpool_limits
     from oracle import ddrl_oracle as O
     from ddrl_amd.spec import make_cfg
     cfg, inst = make_cfg(env, n_envs, T)
     rng = np.random.default_rng(seed)
-    P, A = cfg.n_policies, cfg.act_dim
-    agents = list(inst.agent_names)
-    params = [O.ffn_init(rng, cfg.obs_dim[p], 2 * A) for p in range(P)]
-    shapes = [O.ffn_param_shapes(cfg.obs_dim[p], 2 * A) for p in range(P)]
-    obs = rng.normal(size=(T + 1, n_envs, cfg.obs_full_dim)).astype(np.float32)
-    eps = rng.normal(size=(T, n_envs, cfg.n_agents, A)).astype(np.float32)
-    fw = rng.normal(size=(T, n_envs)).astype(np.float32)
-    cfrc = rng.normal(size=(T, n_envs, 14, 6)).astype(np.float32)
     with threadpool_limits(limits=threads):
         t0 = time.perf_counter()
-        rs = O.RunningStat((cfg.obs_full_dim,))
-        rec = [dict(obs=[], act=[], logits=[], logp=[], vf=[]) for _ in range(P)]
-        rew = np.zeros((P, T, n_envs), np.float32)
-        tables = {a: inst.contact_force_indices[a] for a in agents}
-        z = O.mean_std_filter(obs[0], rs, True, 10.0)
-        for t in range(T):
-            actions = np.zeros((n_envs, 8))
-            for p in range(P):
-                a_name = agents[p]
-                x = z[:, inst.obs_indices[a_name]].astype(np.float32)
-                logits, value, _ = O.ffn_forward(params[p], x)
-                act = O.dg_sample(logits, eps[t, :, p])
-                for k, v in (("obs", x), ("act", act), ("logits", logits),
-                             ("logp", O.dg_logp(logits, act)), ("vf", value)):
-                    rec[p][k].append(v)
-                actions[:, inst.action_indices[a_name]] = np.clip(act, -1, 1)
-            for e in range(n_envs):
-                ad = {a: actions[e, inst.action_indices[a]] for a in agents}
-                rw = O.per_leg_reward(float(fw[t, e]), cfrc[t, e], ad, tables, 0.5, 0.05)
-                for p in range(P):
-                    rew[p, t, e] = rw[agents[p]]
-            z = O.mean_std_filter(obs[t + 1], rs, True, 10.0)
-        for p in range(P):
-            r = {k: np.stack(v) for k, v in rec[p].items()}
-            r["rew"] = rew[p]
-            last_v = O.ffn_forward(params[p], z[:, inst.obs_indices[agents[p]]].astype(np.float32))[1]
-            adv, vt = O.gae_fragment(r["rew"], r["vf"], np.zeros((T, n_envs), bool), last_v)
-            adv, _, _ = O.standardize(adv.reshape(-1))
-            R = T * n_envs
-            batch = dict(obs=r["obs"].reshape(R, -1), actions=r["act"].reshape(R, -1),
-                         logits=r["logits"].reshape(R, -1), logp=r["logp"].reshape(-1),
-                         vf_preds=r["vf"].reshape(-1), adv=adv, vt=vt.reshape(-1))
-            sh, pe = O.sgd_schedule(rng, R, 128, 10)
-            adam = O.Adam(sum(int(np.prod(s)) for _, s in shapes[p]))
-            O.ppo_update("ffn", params[p], shapes[p], adam, batch, sh, pe, np.float32(0.2), {})
+        batches = _cpu_rollout(O, cfg, inst, n_envs, T, rng)
+        for p in range(cfg.n_policies):
+            _cpu_update(O, cfg, p, batches[p], rng)
         dt = time.perf_counter() - t0
+    R = len(batches[0]["adv"])
     return T * n_envs / dt, dt, f"{env}: {n_envs} envs x T={T} (full iteration: rollout, GAE, " \
-                                f"10 x {T * n_envs // 128} minibatches x {P} policies)"
+                                f"{cfg.num_sgd_iter} x {R // 128} minibatches x {cfg.n_policies} " \
+                                f"{'GraphNet' if cfg.model_kind == 1 else 'fcnet'} polic" \
+                                f"{'y' if cfg.n_policies == 1 else 'ies'})"
 
 
 def _cpu_rollout_chunk(a):
     """One rollout worker of the parallel CPU baseline: its own envs and its own env-side
-    MeanStdFilter (as every RLlib rollout worker process has), T steps, then GAE per policy."""
+    MeanStdFilter, T steps, then GAE per policy."""
     env, n_envs, T, seed = a
     from threadpoolctl import threadpool_limits
     from oracle import ddrl_oracle as O
     from ddrl_amd.spec import make_cfg
     with threadpool_limits(limits=1):
         cfg, inst = make_cfg(env, n_envs, T)
-        rng = np.random.default_rng(seed)
-        P, A = cfg.n_policies, cfg.act_dim
-        agents = list(inst.agent_names)
-        params = [O.ffn_init(np.random.default_rng(1000 + p), cfg.obs_dim[p], 2 * A) for p in range(P)]
-        obs = rng.normal(size=(T + 1, n_envs, cfg.obs_full_dim)).astype(np.float32)
-        eps = rng.normal(size=(T, n_envs, cfg.n_agents, A)).astype(np.float32)
-        fw = rng.normal(size=(T, n_envs)).astype(np.float32)
-        cfrc = rng.normal(size=(T, n_envs, 14, 6)).astype(np.float32)
-        rs = O.RunningStat((cfg.obs_full_dim,))
-        rec = [dict(obs=[], act=[], logits=[], logp=[], vf=[]) for _ in range(P)]
-        rew = np.zeros((P, T, n_envs), np.float32)
-        tables = {a: inst.contact_force_indices[a] for a in agents}
-        z = O.mean_std_filter(obs[0], rs, True, 10.0)
-        for t in range(T):
-            actions = np.zeros((n_envs, 8))
-            for p in range(P):
-                x = z[:, inst.obs_indices[agents[p]]].astype(np.float32)
-                logits, value, _ = O.ffn_forward(params[p], x)
-                act = O.dg_sample(logits, eps[t, :, p])
-                for k, v in (("obs", x), ("act", act), ("logits", logits), ("logp", O.dg_logp(logits, act)),
-                             ("vf", value)):
-                    rec[p][k].append(v)
-                actions[:, inst.action_indices[agents[p]]] = np.clip(act, -1, 1)
-            for e in range(n_envs):
-                ad = {a: actions[e, inst.action_indices[a]] for a in agents}
-                rw = O.per_leg_reward(float(fw[t, e]), cfrc[t, e], ad, tables, 0.5, 0.05)
-                for p in range(P):
-                    rew[p, t, e] = rw[agents[p]]
-            z = O.mean_std_filter(obs[t + 1], rs, True, 10.0)
-        out = []
-        for p in range(P):
-            r = {k: np.stack(v) for k, v in rec[p].items()}
-            last_v = O.ffn_forward(params[p], z[:, inst.obs_indices[agents[p]]].astype(np.float32))[1]
-            adv, vt = O.gae_fragment(rew[p], r["vf"], np.zeros((T, n_envs), bool), last_v)
-            R = T * n_envs
-            out.append(dict(obs=r["obs"].reshape(R, -1), actions=r["act"].reshape(R, -1),
-                            logits=r["logits"].reshape(R, -1), logp=r["logp"].reshape(-1),
-                            vf_preds=r["vf"].reshape(-1), adv=adv.reshape(-1), vt=vt.reshape(-1)))
-    return out
+        return _cpu_rollout(O, cfg, inst, n_envs, T, np.random.default_rng(seed))
 
 
 def _cpu_update_policy(a):
-    """One policy's minibatch SGD chain over the union batch (10 epochs; sequential by
-    construction: every step needs the previous step's weights)."""
+    """One policy's minibatch SGD chain over the union batch."""
     env, p, batch, seed = a
     from threadpoolctl import threadpool_limits
     from oracle import ddrl_oracle as O
     from ddrl_amd.spec import make_cfg
     with threadpool_limits(limits=1):
         cfg, _ = make_cfg(env, 1, 1)
-        A = cfg.act_dim
-        params = O.ffn_init(np.random.default_rng(1000 + p), cfg.obs_dim[p], 2 * A)
-        shapes = O.ffn_param_shapes(cfg.obs_dim[p], 2 * A)
-        adv, _, _ = O.standardize(batch["adv"])
-        sh, pe = O.sgd_schedule(np.random.default_rng(seed), len(adv), 128, 10)
-        adam = O.Adam(sum(int(np.prod(s)) for _, s in shapes))
-        O.ppo_update("ffn", params, shapes, adam, dict(batch, adv=adv), sh, pe, np.float32(0.2), {})
+        _cpu_update(O, cfg, p, batch, np.random.default_rng(seed))
     return p
 
 
@@ -508,10 +528,20 @@ def main():
     flops_launch = flops_row * rows_per_step * steps_per_policy * P
     achieved_tf = flops_launch / (upd_avg_ms * 1e-3) / 1e12
     ks1 = (d + 3) // 4
+    # the GNN gradient launch reduces over its tiles in its own tail when it covers a full
+    # 128-row minibatch (32 tiles per combination) and DDRL_GNN_TAIL is not 0 (gnn.hip
+    # launch_step_gnn: ga.tail); the fused step then also runs clip + Adam there
+    gnn_tail = os.environ.get("DDRL_GNN_TAIL", "1") != "0" and rows_per_step == 128
+    pkey = pmc_key(args.env, gnn_tail)
     if gnn:
-        kernel = ("k_gnn<GRAD> + k_gnn_reduce + k_gnn_adam (three launches per minibatch step)"
-                  if os.environ.get("DDRL_GNN_TAIL", "1") == "0" or ddp else
-                  "k_gnn<GRAD> with the reduction and clip + Adam in its tail (one launch per minibatch step)")
+        if ddp:
+            coll = "RCCL" if backend == "nccl" else backend
+            kernel = (f"k_gnn<GRAD> (reduction in its tail) + {coll} all-reduce + k_apply_adam per minibatch step"
+                      if gnn_tail else
+                      f"k_gnn<GRAD> + k_gnn_reduce + {coll} all-reduce + k_apply_adam per minibatch step")
+        else:
+            kernel = ("k_gnn<GRAD> with the reduction and clip + Adam in its tail (one launch per minibatch step)"
+                      if gnn_tail else "k_gnn<GRAD> + k_gnn_reduce + k_gnn_adam (three launches per minibatch step)")
         # (tiles of 4 graphs) x (actor, critic) x 4 backward shares (gnn.hip GNN_Z), one per CU
         active_cus = min(256, 2 * ((rows_per_step + 3) // 4) * 4)
         model = f"shared GraphNet/MPNN leg policy (4 nodes x 19 features + ego quaternion, A={A})"
@@ -528,13 +558,15 @@ def main():
     # algorithmic HBM bytes: each minibatch row's record fields read once per branch
     # (policy: obs, action, old logits, logp, adv; value: obs, vf, vt) + its shuffle index.
     # The fcnet launch keeps theta / Adam m, v on chip for the whole launch (LDS + registers),
-    # so its per-step bytes are the records; the GNN step is three launches, so every step also
-    # reads and writes theta, m, v (6 x 4 B per parameter) and writes + reads one gradient
-    # (2 x 4 B per parameter)
+    # so its per-step bytes are the records.  A GNN step is a launch of its own (one, with the
+    # reduction and Adam in its tail), so every step also reads and writes theta, m, v (6 x 4 B
+    # per parameter); where the summed gradient goes through memory (three launches, or the
+    # data-parallel all-reduce) it is written and read once more (2 x 4 B per parameter)
     obs_len = 93 if gnn else d
     rec_bytes_launch = 4 * (2 * obs_len + 3 * A + 4 + 2) * rows_per_step * steps_per_policy * P
     if gnn:
-        rec_bytes_launch += (6 + 2) * 4 * ctx.n_params[0] * steps_per_policy * P
+        grad_io = 0 if (gnn_tail and not ddp) else 2
+        rec_bytes_launch += (6 + grad_io) * 4 * ctx.n_params[0] * steps_per_policy * P
     ddp_how = ("RCCL all-reduce of the gradient every SGD step, loop in the library (ddrl_ppo_update_ddp)"
                if isinstance(learner, NativeDataParallelLearner) else
                f"{'RCCL' if backend == 'nccl' else backend} all-reduce of the gradient every SGD step, Python loop") \
@@ -572,19 +604,20 @@ def main():
             "kernel": kernel,
             "bound": "mfma", "achieved": achieved_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved_tf / PEAK_FP32_TFLOPS,
-            "traffic": None if ddp else pmc_traffic(args.env, steps_per_policy * P),
-            "traffic_source": None if ddp else f"{pmc_summary()[1]} (bytes per step x steps of this update)",
+            "traffic": None if ddp else pmc_traffic(pkey, steps_per_policy * P),
+            "traffic_source": None if ddp else f"{pmc_summary(pkey)[1]} [{pkey}] (bytes per step x steps of this update)",
             "algorithmic_flops_per_launch": flops_launch,
             "algorithmic_bytes_per_launch": rec_bytes_launch,
             "active_cus": active_cus,
             "frac_of_active_cus": achieved_tf / (PEAK_FP32_TFLOPS * active_cus / 256),
-            **({} if ddp else pmc_mfma(args.env)),
+            **({} if ddp else pmc_mfma(pkey)),
         },
     }
     if pcie is not None:
         result["pcie_inclusive"] = pcie
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not gnn:
-        v, dt, sample = cpu_baseline(args.env, args.cpu_envs, T)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu_envs = cpu_sample_envs(args.env, args.cpu_envs)
+        v, dt, sample = cpu_baseline(args.env, cpu_envs, T)
         result["cpu_baseline"] = {"value": v, "unit": "env-steps/s", "cores": 1, "kind": "port",
                                   "sample": sample + f"; {dt:.1f} s", "host_cpus": os.cpu_count()}
         # the same sample on this job's share of the host cores (OMP_NUM_THREADS
@@ -594,7 +627,7 @@ def main():
         nthr = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count())
         import subprocess
         code = ("import json, bench; v, dt, w = bench.cpu_baseline_parallel(%r, %d, %d, %d); "
-                "print(json.dumps([v, dt, w]))" % (args.env, args.cpu_envs, T, nthr))
+                "print(json.dumps([v, dt, w]))" % (args.env, cpu_envs, T, nthr))
         r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600,
                            cwd=os.path.dirname(os.path.abspath(__file__)))
         if r.returncode == 0:
@@ -602,7 +635,8 @@ def main():
             result["cpu_baseline_all_cores"] = {
                 "value": v2, "unit": "env-steps/s", "cores": w2, "kind": "port",
                 "sample": f"same sample on {w2} worker processes: rollout over env chunks, update over the "
-                          f"{ctx.cfg.n_policies} policies; {dt2:.1f} s"}
+                          f"{ctx.cfg.n_policies} polic{'y' if ctx.cfg.n_policies == 1 else 'ies'} (each "
+                          f"policy's minibatch chain is sequential); {dt2:.1f} s"}
         else:
             result["cpu_baseline_all_cores"] = {"error": r.stderr[-300:]}
     if rank == 0:

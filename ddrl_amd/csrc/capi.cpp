@@ -120,6 +120,17 @@ static int dalloc(ddrl_ctx* c, T** p, size_t count) {
   return 0;
 }
 
+// a buffer that is replaced by a larger one (the data-parallel loop's chunk and slots): the
+// callers run after a stream synchronize, so nothing in flight still reads it
+template <class T>
+static void dfree(ddrl_ctx* c, T** p) {
+  if (!*p) return;
+  auto it = std::find(c->allocs.begin(), c->allocs.end(), static_cast<void*>(*p));
+  if (it != c->allocs.end()) c->allocs.erase(it);
+  (void)hipFree(*p);
+  *p = nullptr;
+}
+
 static RecLayout make_layout(const ddrl_cfg& cfg, int d) {
   RecLayout L;
   const int A = cfg.act_dim;
@@ -263,12 +274,15 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
     c->gnn.grad = c->pol[0].grad;
     rc = dalloc(c, &c->gnn.part, (size_t)(DDRL_MB / 4) * c->gnn.part_stride) || dalloc(c, &c->gnn.statp, 2 * (DDRL_MB / 4) * 8) ||
          dalloc(c, &c->gnn.normp, (np + 255) / 256) || dalloc(c, &c->gnn.bp_cur, 2) || dalloc(c, &c->gnn.flags, 256) ||
-         dalloc(c, &c->gnn.gran, 256) || dalloc(c, &c->gnn.plist, np);
+         dalloc(c, &c->gnn.gran, 256) || dalloc(c, &c->gnn.plist, np) || dalloc(c, &c->gnn.xcc, 256);
     c->gnn.seq = 0;
     c->gnn.lists = 0;
     c->gnn.err = c->err;
     c->gnn.tail = 1;
+    c->gnn.xcc_pending = 0;
+    c->gnn.misplace = 0;
     if (const char* e = std::getenv("DDRL_GNN_TAIL")) c->gnn.tail = std::atoi(e) != 0;
+    if (const char* e = std::getenv("DDRL_TEST_GNN_MISPLACE")) c->gnn.misplace = std::atoi(e) != 0;
     // the record chunk of the fused update is allocated by the first ddrl_ppo_update (forward-only
     // and data-parallel contexts never need it), sized to the schedule when that is shorter
     c->gnn.chunk = nullptr;
@@ -352,17 +366,40 @@ static int placement_broken(ddrl_ctx* c) {
   return bad;
 }
 
+// The one-launch GNN step needs the 32 tiles of each (net, backward share) combination on one
+// XCD (gnn.hip gnn_tail).  Returns 1 if the last such launch's per-tile XCC record breaks that.
+static int gnn_placement_broken(ddrl_ctx* c) {
+  if (c->cfg.model_kind != DDRL_MODEL_GNN || !c->gnn.xcc_pending) return 0;
+  c->gnn.xcc_pending = 0;
+  int x[256] = {0};
+  if (hipMemcpy(x, c->gnn.xcc, sizeof(x), hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  int bad = 0;
+  for (int k = 0; k < 8; ++k)
+    for (int t = 1; t < DDRL_MB / 4; ++t) bad |= x[32 * k + t] != x[32 * k];
+  return bad;
+}
+
 static int check_err(ddrl_ctx* c) {
   int e = 0;
   HIPCHK(hipMemcpy(&e, c->err, sizeof(int), hipMemcpyDeviceToHost));
   if (e) {
     (void)hipMemset(c->err, 0, sizeof(int));
-    // a one-launch GNN step whose waits were abandoned (e.g. a broken XCD placement): the
-    // context goes on with the three-launch step
-    if (c->cfg.model_kind == DDRL_MODEL_GNN) c->gnn.tail = 0;
     const int bad = placement_broken(c);
+    const int gbad = gnn_placement_broken(c);
     if (restore_snapshot(c)) return -1;
     c->snap_mask = 0;
+    if (c->cfg.model_kind == DDRL_MODEL_GNN) {
+      // a one-launch GNN step whose waits were abandoned or refused a flag from another XCD:
+      // the context goes on with the three-launch step (no cross-workgroup waits)
+      const int was_tail = c->gnn.tail;
+      c->gnn.tail = 0;
+      return fail(std::string("GraphNet update: ") +
+                  (gbad ? "the workgroups of a (net, backward share) combination ran on different XCDs (placement "
+                          "check), so the one-launch step's reduction through the XCD's L2 was refused"
+                        : "a wait between workgroups was abandoned (3 s timeout or a failed launch)") +
+                  ".  The weights, Adam state and beta powers are as before the call" +
+                  (was_tail ? "; this context has switched to the three-launch step: call the update again" : ""));
+    }
     if (bad && !c->xchg_atomic) {
       c->xchg_atomic = 1;
       return fail("update kernel: the workgroups of a policy ran on different XCDs (placement check), so the "
@@ -377,6 +414,9 @@ static int check_err(ddrl_ctx* c) {
   // memory) gave correct results -- the tags admit only this step's data -- but the next
   // launch might not be so lucky: switch protocols now
   if (placement_broken(c)) c->xchg_atomic = 1;
+  // the GNN reducers accept flags only from their own XCD, so a step that completed had its
+  // combinations in place; a record that says otherwise still ends the one-launch steps
+  if (gnn_placement_broken(c)) c->gnn.tail = 0;
   c->snap_mask = 0;
   return 0;
 }
@@ -1033,11 +1073,16 @@ int ddrl_ppo_update_ddp(ddrl_ctx* c, int pid, const int32_t* shuffle, const int3
   const int CH = std::min(DDP_CHUNK_STEPS, steps);
   const int stride = P.lay.stride;
   const size_t need = (size_t)CH * m * stride;
+  // grown buffers replace the old ones (the previous call ended with a stream synchronize)
   if (c->ddp_chunk_n < need) {
+    dfree(c, &c->ddp_chunk);
+    c->ddp_chunk_n = 0;
     if (dalloc(c, &c->ddp_chunk, need)) return -1;
     c->ddp_chunk_n = need;
   }
   if (c->ddp_slots_n < (size_t)steps) {
+    dfree(c, &c->ddp_slots);
+    c->ddp_slots_n = 0;
     if (dalloc(c, &c->ddp_slots, (size_t)steps)) return -1;
     c->ddp_slots_n = (size_t)steps;
   }
@@ -1045,7 +1090,9 @@ int ddrl_ppo_update_ddp(ddrl_ctx* c, int pid, const int32_t* shuffle, const int3
   HIPCHK(hipMemcpyAsync(c->ddp_slots, c->ddp_slots_host.data(), sizeof(int32_t) * steps, hipMemcpyHostToDevice,
                         c->stream));
   c->kl_last[pid] = kl;
-  if (ffn && snapshot(c, 1 << pid)) return -1;   // restored by check_err if any step fails
+  // restored by check_err if any step fails (the GNN gradient launches of 128 rows per rank
+  // reduce in their tail, with bounded waits: ADVICE r4)
+  if (snapshot(c, 1 << pid)) return -1;
   for (int s = 0; s < steps; ++s) {
     const int k = s % CH;
     if (k == 0) launch_rows_gather(c->stream, P.rec, stride, shuffle, c->ddp_slots, m, s, std::min(CH, steps - s),

@@ -832,7 +832,11 @@ __global__ void __launch_bounds__(256) k_gnn(GnnArgs ga) {
   int tile, net, zs;
   if (MODE == GNN_GRAD && ga.xgrid) {
     const int b = blockIdx.x;
-    tile = b >> 3; net = (b >> 2) & 1; zs = b & 3;
+    if (ga.xgrid == 2) {   // test hook (DDRL_TEST_GNN_MISPLACE): combination k = b / 32 straddles every XCD
+      tile = b & 31; net = (b >> 7) & 1; zs = (b >> 5) & 3;
+    } else {
+      tile = b >> 3; net = (b >> 2) & 1; zs = b & 3;
+    }
   } else {
     tile = blockIdx.x; net = blockIdx.y; zs = blockIdx.z;
   }
@@ -991,9 +995,11 @@ __global__ void __launch_bounds__(256) k_gnn_adam(GnnArgs ga, int nred, int n) {
 // combination's partials are all written -- plain stores into the XCD's L2 -- and read on one
 // XCD:
 //   * each workgroup, once its partials and loss statistics are in L2 (s_waitcnt), raises its
-//     arrival flag (flag[b] = this launch's tag);
+//     arrival flag (flag[32 k + tile] = this launch's tag and the workgroup's XCC id, agent
+//     scope) and records its XCC for the host's placement check;
 //   * tiles r < R_k of combination k are also its reduction blocks: reducer r waits for the 32
-//     flags of its combination (one per thread, sc1 polls: they miss the CU's own L1), sums
+//     flags of its combination (one per thread, sc1 polls: they miss the CU's own L1; a flag of
+//     this launch from another XCD raises the error word, gnn_wait_flag), sums
 //     the 32 partials of 256 owned parameters in tile order with sc1 loads (the three-launch
 //     reduction's order, so the gradient is bit-identical) and publishes its norm^2 partial as
 //     a tagged granule {value, tag} with a device-scope atomic store (the one value that crosses
@@ -1007,9 +1013,30 @@ __global__ void __launch_bounds__(256) k_gnn_adam(GnnArgs ga, int nred, int n) {
 // every partial written through to memory + one arrival counter 22.7 us per step (256 arrivals
 // on one device-scope atomic serialize, MI355X_MICROARCH.md "fanin"), flags 21.5, release /
 // acquire 33.1, against 18.9 for three launches.
-__device__ __forceinline__ bool gnn_wait_flag(const GnnArgs& ga, const unsigned* flag, unsigned long long t0) {
+// Placement guard: a flag carries its writer's XCC id (HW_REG_XCC_ID) below the tag, and a
+// reducer accepts a flag of this launch only from its own XCD.  A flag of this launch from
+// another XCD means the combination straddles XCDs, so its partials may still sit in the other
+// XCD's L2: the reducer raises the error word instead of summing them (the host restores its
+// snapshot and the context goes on with three launches).  Flags are stored at agent scope
+// (written through), so a writer on another XCD is seen -- and refused -- at once rather than
+// after the wait's bound.
+#ifndef DDRL_GNN_FLAG_AGENT
+#define DDRL_GNN_FLAG_AGENT 1
+#endif
+__device__ __forceinline__ unsigned gnn_xcc() {
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & 0xfu;
+}
+__device__ __forceinline__ bool gnn_wait_flag(const GnnArgs& ga, const unsigned* flag, unsigned xcc,
+                                              unsigned long long t0) {
   for (;;) {
-    if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ga.tag) return true;
+    const unsigned f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((f >> 4) == ga.tag) {
+      if ((f & 0xfu) == xcc) return true;
+      __hip_atomic_store(ga.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // misplaced combination
+      return false;
+    }
     const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
     if ((dt > 20000ull && __hip_atomic_load(ga.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) || dt > 300000000ull) {
       __hip_atomic_store(ga.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1039,13 +1066,20 @@ __device__ __forceinline__ float sc1_ld(const float* p) {
 }
 
 __device__ __forceinline__ void gnn_tail(const GnnArgs& ga, float* lds, int tile, int net, int zs) {
-  const int b = blockIdx.x, k = b & 7, tid = threadIdx.x;
+  const int k = 4 * net + zs, tid = threadIdx.x;   // combination (net, share)
+  const unsigned xcc = gnn_xcc();
   // LDS of the finished tile, reused: [0..3] norm^2 of the waves, [4..5] beta powers,
   // [8..12] loss statistics, [16] clip scale, [17] ok, [64 ..] granule values
   float* T = lds;
   __builtin_amdgcn_s_waitcnt(0);   // this wave's partial / statistics stores are in L2
   __syncthreads();
-  if (tid == 0) __hip_atomic_store(ga.flags + b, ga.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  // arrival flag of tile `tile` of combination k: this launch's tag and this workgroup's XCC;
+  // the placement record for the host check (capi.cpp gnn_placement_broken)
+  if (tid == 0) {
+    __hip_atomic_store(ga.flags + 32 * k + tile, (ga.tag << 4) | xcc, __ATOMIC_RELAXED,
+                       DDRL_GNN_FLAG_AGENT ? __HIP_MEMORY_SCOPE_AGENT : __HIP_MEMORY_SCOPE_WORKGROUP);
+    ga.xcc[32 * k + tile] = (int)xcc;
+  }
   const int m = ga.poff[k + 1] - ga.poff[k];
   const int r = tile;   // reducer r of combination k: parameters plist[poff[k] + 256 r ..]
   const int R = (m + 255) / 256;
@@ -1067,7 +1101,7 @@ __device__ __forceinline__ void gnn_tail(const GnnArgs& ga, float* lds, int tile
   }
   // the combination's 32 workgroups have arrived (one flag per thread)
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  const bool ok = tid >= ga.ntiles || gnn_wait_flag(ga, ga.flags + 8 * tid + k, t0);
+  const bool ok = tid >= ga.ntiles || gnn_wait_flag(ga, ga.flags + 32 * k + tid, xcc, t0);
   if (!__syncthreads_and(ok)) return;
   if (stats) {
     if (tid < 5) {   // all 32 loads in flight (all 32 tiles on this path), then summed in tile order
@@ -1239,9 +1273,28 @@ static GnnArgs grad_args(const UpdateArgs& u, const UpdateHyper& h, int step, in
 // other shares idle, over a partial row pre-filled with a NaN pattern no computed value has.
 // Every parameter must be owned by exactly one share, and each (net, share) combination's list
 // must fit the reducers its 32 tiles provide; otherwise the context keeps three launches.
+// The one-launch step's waits need every workgroup of the 256-block grid resident at once, with
+// a combination's 32 workgroups on one XCD: at least 32 blocks per XCD must fit.
+static bool gnn_tail_resident(int layer) {
+  const void* f = nullptr;
+  switch (layer) {
+    case DDRL_GNN_GCN: f = reinterpret_cast<const void*>(&k_gnn<2, GNN_GRAD, DDRL_GNN_GCN>); break;
+    case DDRL_GNN_MPNN2: f = reinterpret_cast<const void*>(&k_gnn<2, GNN_GRAD, DDRL_GNN_MPNN2>); break;
+    case DDRL_GNN_GAT1: f = reinterpret_cast<const void*>(&k_gnn<2, GNN_GRAD, DDRL_GNN_GAT1>); break;
+    default: f = reinterpret_cast<const void*>(&k_gnn<2, GNN_GRAD, DDRL_GNN_MPNN>); break;
+  }
+  int dev = 0, per_cu = 0;
+  hipDeviceProp_t pr;
+  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&pr, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, 0) != hipSuccess)
+    return false;
+  return per_cu >= 1 && per_cu * (pr.multiProcessorCount / 8) >= DDRL_MB / 4 && per_cu * pr.multiProcessorCount >= 256;
+}
+
 static void gnn_build_owner_lists(hipStream_t s, const UpdateArgs& u, const UpdateHyper& h, float inv_n,
                                   GnnScratch& sc, int layer) {
   sc.lists = -1;
+  if (!gnn_tail_resident(layer)) return;
   GnnArgs ga = grad_args(u, h, 0, 4, inv_n, sc, nullptr, layer);
   const int n = ga.n_params;
   const int actor = gnn_net_off(u.A, 1, layer).wenc;   // first critic parameter
@@ -1289,9 +1342,12 @@ void launch_step_gnn(hipStream_t s, const UpdateArgs& u, const UpdateHyper& h, i
   if (sc.tail && sc.lists == 0 && ntiles == DDRL_MB / 4 && GNN_Z == 4) gnn_build_owner_lists(s, u, h, inv_n, sc, layer);
   ga.tail = sc.tail && sc.lists == 1 && ntiles == DDRL_MB / 4 && GNN_Z == 4;
   if (ga.tail) {
-    if (++sc.seq == 0) sc.seq = 1;   // tags never 0 (the buffers start zeroed)
+    sc.seq = (sc.seq + 1) & 0x0FFFFFFFu;   // 28-bit tags (the flags hold tag << 4 | XCC id)
+    if (sc.seq == 0) sc.seq = 1;           // tags never 0 (the buffers start zeroed)
     ga.tag = sc.seq;
-    ga.xgrid = 1;
+    ga.xgrid = sc.misplace ? 2 : 1;
+    ga.xcc = sc.xcc;
+    sc.xcc_pending = 1;
     ga.plist = sc.plist;
     for (int k = 0; k < 9; ++k) ga.poff[k] = sc.poff[k], ga.rbase[k] = sc.rbase[k];
     GNN_LAUNCH(GNN_GRAD, layer, dim3(ntiles * 8), s, ga);

@@ -272,6 +272,9 @@ extern "C" int ddrl_hostenv_create(int n_envs, int obs_dim, int n_threads, uint6
   h->seed = seed;
   h->tv_list.assign(1, (double)target_velocity);
   h->st.assign(n_envs, EnvState{});
+  // the create-time velocity until the first reset draws one (a step before any reset must not
+  // divide by zero in the TVel reward)
+  for (auto& s : h->st) s.tv = (double)target_velocity;
   const size_t N = n_envs;
   // pinned when a GPU is present (the DMA engines read / write them directly); without one
   // (CPU tests of the env plane) ordinary aligned host memory

@@ -193,7 +193,9 @@ struct GnnArgs {
   // tag; the XCD-grouped 1-D grid (xgrid); the parameters of each (net, share) combination
   // (plist[poff[k] .. poff[k + 1]), k = 4 net + share) and the first reducer index of each (rbase)
   unsigned* flags; unsigned long long* gran; unsigned tag; int tail; int nred; int n_params; int ntiles; int* err;
-  int xgrid; int only_share; const int* plist; int poff[9]; int rbase[9];
+  // xgrid: 1 = the XCD-grouped grid, 2 = test hook remapping each combination across every XCD;
+  // xcc: [8 combinations][32 tiles] XCC id of the workgroup that ran each tile (placement record)
+  int xgrid; int only_share; const int* plist; int poff[9]; int rbase[9]; int* xcc;
 };
 struct GnnScratch {
   float* part; int part_stride; float* statp; float* normp; float* bp_cur; float* grad;
@@ -207,6 +209,9 @@ struct GnnScratch {
   int lists;                    // 0: not built yet, 1: built, -1: unusable (three launches)
   int tail;           // 1: reduction + clip + Adam in the gradient launch (DDRL_GNN_TAIL, default 1)
   int* err;           // the context's error word
+  int* xcc;           // [256] XCC id per (combination, tile) of the last one-launch step (device)
+  int xcc_pending;    // a one-launch step ran since the host last checked its placement
+  int misplace;       // test hook (DDRL_TEST_GNN_MISPLACE): every combination straddles the XCDs
 };
 #define GNN_CHUNK_STEPS 1024
 int gnn_param_total(int A, int layer);   // layer: DDRL_GNN_*
