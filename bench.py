@@ -283,6 +283,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) iteration")
     ap.add_argument("--cpu-envs", type=int, default=512)
+    ap.add_argument("--sgd-iter", type=int, default=None,
+                    help="profiling aid: num_sgd_iter of the run (default: the config's 10 epochs)")
     ap.add_argument("--ddp-mode", default="split", choices=["split", "local"],
                     help="shared-policy envs on N>1 GPUs: per-rank rows per SGD step (see ddrl_amd/ddp.py); "
                          "split (default) = the reference's 128-row minibatch SGD, local = 128 rows per rank")
@@ -324,7 +326,8 @@ def main():
 
     n_local = args.envs // world + (1 if rank < args.envs % world else 0)
     T = args.frag
-    cfg, inst = make_cfg(args.env, n_local, T)
+    run_config = {"num_sgd_iter": args.sgd_iter} if args.sgd_iter else None
+    cfg, inst = make_cfg(args.env, n_local, T, run_config)
     stream = torch.cuda.current_stream()
     ctx = N.Context(cfg, local, stream.cuda_stream)
     P, A = cfg.n_policies, cfg.act_dim
@@ -350,7 +353,7 @@ def main():
     uctx = None
     if gather:
         # the learner context: the union batch of all ranks (rank-major), same weights everywhere
-        ucfg, _ = make_cfg(args.env, n_local * world, T)
+        ucfg, _ = make_cfg(args.env, n_local * world, T, run_config)
         uctx = N.Context(ucfg, local, stream.cuda_stream)
         for p in range(P):
             uctx.params_set(p, ctx.params_get(p))

@@ -12,12 +12,23 @@
 // k-step (fb, r)); the A operand (weights) is then read with the same permuted k.  So a
 // whole MLP runs from registers with one LDS read per MFMA for the weights.
 //
-// LDS matrices with 64 columns are stored row-major, 64 floats per row, with the column
-// XOR-swizzled by the row:  col' = col ^ swz(row),  swz(row) = ((row >> 1) & 7) << 1.
-// The XOR only touches bits 1..3, so it never moves a column out of its 16-column block
-// and every MFMA operand address is  (per-lane base) + (compile-time immediate):
-//   "R" reads  (row = 4s + q, col = 16t + c): forward weights, dW operands -> 2-way at most
-//   "W" access (row = 16u + c, col = 16t + 4q + r): activation stores, W2^T reads -> 2-way
+// LDS matrices with 64 columns are stored row-major with the column XOR-swizzled by the row
+// inside its 16-column block (col' = col ^ swz(row), swz < 16), so every MFMA operand address
+// is  (per-lane base) + (compile-time immediate).  A ds_read_b32 serves a wave in two groups of
+// 32 lanes over 32 banks ((address / 4) mod 32), and every pattern below puts two 16-lane
+// halves of a group on two different rows:
+//   "R" reads  (row = 4s + q, col = 16t + c): forward weights, dW operands (rows 1 apart)
+//   "W" access (row = 16u + c, col = 16t + 4q + r): activation stores, W2^T reads
+//   "E" access (row = 16u + 4q + r, col = 16t + c): Adam's weights (rows 4 apart)
+// Round 5 (DDRL_LDS_PAD, default 1): rows are DDRL_LRS = 80 floats apart (a
+// stride of 16 banks) and row r starts 16 ((r >> 2) & 1) floats into its slot, so rows r and
+// r + 1 and rows r and r + 4 start in opposite 16-bank halves; swz(row) = row & 0xB then makes
+// the 8 rows of each half of a "W" group cover all 16 (col ^ swz) banks of the half: all three
+// patterns are conflict-free.  The round-4 layout (64 floats per row, swz = ((row >> 1) & 7) << 1)
+// left every one of them 2-way conflicted (SQ_LDS_BANK_CONFLICT 2.1x SQ_ACTIVE_INST_LDS).  The
+// layout is a template parameter (PAD) of the helpers below, defaulting to DDRL_LDS_PAD: the
+// fused update's A = 8 kernel without the row split keeps the compact one (its LDS budget has no
+// room for the 25 % larger images).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -31,8 +42,21 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 #endif
 #define DDRL_LOG2PI 1.8378770664093453
 
-__device__ __forceinline__ int swz(int row) { return ((row >> 1) & 7) << 1; }
-__device__ __forceinline__ int sidx(int row, int col) { return row * 64 + (col ^ swz(row)); }
+#ifndef DDRL_LDS_PAD
+#define DDRL_LDS_PAD 1
+#endif
+constexpr bool kLdsPad = DDRL_LDS_PAD != 0;
+__host__ __device__ constexpr int lds_rs(bool pad) { return pad ? 80 : 64; }           // floats per row
+__host__ __device__ constexpr int lds_blk(bool pad) { return 16 * lds_rs(pad); }       // 16 rows
+__host__ __device__ constexpr int lds_img(int rows, bool pad) { return rows * lds_rs(pad); }
+#define DDRL_LBLK lds_blk(kLdsPad)
+#define DDRL_LIMG(rows) lds_img(rows, kLdsPad)
+template <bool PAD = kLdsPad>
+__device__ __forceinline__ int swz(int row) { return PAD ? (row & 0xB) : (((row >> 1) & 7) << 1); }
+template <bool PAD = kLdsPad>
+__device__ __forceinline__ int lrow(int row) { return PAD ? row * 80 + ((row & 4) << 2) : row * 64; }
+template <bool PAD = kLdsPad>
+__device__ __forceinline__ int sidx(int row, int col) { return lrow<PAD>(row) + (col ^ swz<PAD>(row)); }
 
 __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -190,19 +214,21 @@ struct NetLds {
   float* cup;   // update kernel, policy branch of the "cup" model: leg-coupling table [4][A]
 };
 
-// Per-lane LDS bases for the "R" pattern (row = 4s + q): rbase(v) = (4v + q)*64 + (c ^ swz),
-// valid for every s with s & 3 == v; the address of (s, block t) is
-//   rbase(s & 3) + 1024 * (s >> 2) + 16 * t.
+// Per-lane LDS bases for the "R" pattern (row = 4s + q): rbase(v) = sidx(4v + q, c), valid for
+// every s with s & 3 == v; the address of (s, block t) is
+//   rbase(s & 3) + DDRL_LBLK * (s >> 2) + 16 * t.
+template <bool PAD = kLdsPad>
 __device__ __forceinline__ int rbase(int v) {
   const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
   const int row = 4 * v + q;
-  return row * 64 + (c ^ swz(row));
+  return lrow<PAD>(row) + (c ^ swz<PAD>(row));
 }
 // Per-lane LDS bases for the "W" pattern (row = 16u + c, col = 16t + 4q + r):
-//   wbase(r) = c*64 + ((4q + r) ^ swz(c)); address of (u, t) = wbase(r) + 1024 u + 16 t.
+//   wbase(r) = sidx(c, 4q + r); address of (u, t) = wbase(r) + DDRL_LBLK u + 16 t.
+template <bool PAD = kLdsPad>
 __device__ __forceinline__ int wbase(int r) {
   const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
-  return c * 64 + ((4 * q + r) ^ swz(c));
+  return lrow<PAD>(c) + ((4 * q + r) ^ swz<PAD>(c));
 }
 
 // Forward of one branch for RT row tiles (16 rows each) of this wave.
@@ -210,9 +236,10 @@ __device__ __forceinline__ int wbase(int r) {
 //   KS1       : k-steps of layer 1 (ceil(d / 4)); W1 rows beyond d are zero in LDS
 // Outputs h1[t][4], h2[t][4] (transposed activation tiles), out[t][O] (same in the 4 q-lanes).
 // Every weight operand read from LDS feeds RT MFMAs.
-template <int O, int KS1, int RT>
+template <int O, int KS1, int RT, bool PAD = kLdsPad>
 __device__ __forceinline__ void ffn_fwd_rt(const NetLds& W, const float (*xop)[12],
                                            floatx4 (*h1)[4], floatx4 (*h2)[4], float (*out)[O]) {
+  constexpr int BLK = lds_blk(PAD);
   const int lane = threadIdx.x & 63, q = lane >> 4, c = lane & 15;
 #pragma unroll
   for (int ob = 0; ob < 4; ++ob) {
@@ -224,9 +251,9 @@ __device__ __forceinline__ void ffn_fwd_rt(const NetLds& W, const float (*xop)[1
   // Weight operands of k-step s + 2 are loaded while the MFMAs of step s issue (a 3-deep
   // register ring; the scheduling barrier keeps the compiler from sinking the loads next to
   // their MFMAs, which a single wave per SIMD cannot hide).
-  const int rb[4] = {rbase(0), rbase(1), rbase(2), rbase(3)};
+  const int rb[4] = {rbase<PAD>(0), rbase<PAD>(1), rbase<PAD>(2), rbase<PAD>(3)};
   auto ld1 = [&](int s, float* a) {
-    const float* wp = W.w1 + rb[s & 3] + 1024 * (s >> 2);
+    const float* wp = W.w1 + rb[s & 3] + BLK * (s >> 2);
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob) a[ob] = wp[16 * ob];
   };
@@ -234,10 +261,10 @@ __device__ __forceinline__ void ffn_fwd_rt(const NetLds& W, const float (*xop)[1
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int row = 4 * q + r;
-    fb_base[r] = row * 64 + (c ^ swz(row));
+    fb_base[r] = lrow<PAD>(row) + (c ^ swz<PAD>(row));
   }
   auto ld2 = [&](int k, float* a) {   // k = 4 fb + r
-    const float* wp = W.w2 + fb_base[k & 3] + 1024 * (k >> 2);
+    const float* wp = W.w2 + fb_base[k & 3] + BLK * (k >> 2);
 #pragma unroll
     for (int ob = 0; ob < 4; ++ob) a[ob] = wp[16 * ob];
   };
@@ -343,17 +370,18 @@ __device__ __forceinline__ void head_bwd(const NetLds& W, const float* dout, flo
 }
 
 // dH1^T = W2 . dZ2^T   (MFMA, A = W2[f = 16fb + c][o = 16ob + 4q + r], B = dZ2 tile regs)
-template <int RT>
+template <int RT, bool PAD = kLdsPad>
 __device__ __forceinline__ void layer2_bwd_rt(const NetLds& W, const floatx4 (*dz2)[4], floatx4 (*dh1)[4]) {
+  constexpr int BLK = lds_blk(PAD);
 #pragma unroll
   for (int t = 0; t < RT; ++t)
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) dh1[t][fb] = splat4(0.f);
-  const int wb[4] = {wbase(0), wbase(1), wbase(2), wbase(3)};
+  const int wb[4] = {wbase<PAD>(0), wbase<PAD>(1), wbase<PAD>(2), wbase<PAD>(3)};
   auto ld = [&](int k, float* a) {   // k = 4 ob + r (operands prefetched two steps ahead)
     const float* wp = W.w2 + wb[k & 3] + 16 * (k >> 2);
 #pragma unroll
-    for (int fb = 0; fb < 4; ++fb) a[fb] = wp[1024 * fb];
+    for (int fb = 0; fb < 4; ++fb) a[fb] = wp[BLK * fb];
   };
   float wr[3][4];
   ld(0, wr[0]);
@@ -373,11 +401,11 @@ __device__ __forceinline__ void layer2_bwd(const NetLds& W, const floatx4 dz2[4]
 }
 
 // Write a transposed activation tile set (rows 16*tile + c, features 16fb+4q+r) into an
-// LDS [128][64] swizzled image as row-major activations.
+// LDS swizzled image (DDRL_LIMG(rows) floats) as row-major activations.
 __device__ __forceinline__ void store_act(float* buf, int tile, const floatx4 v[4]) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    float* p = buf + wbase(r) + 1024 * tile;
+    float* p = buf + wbase(r) + DDRL_LBLK * tile;
 #pragma unroll
     for (int fb = 0; fb < 4; ++fb) p[16 * fb] = v[fb][r];
   }
@@ -442,7 +470,7 @@ __device__ __forceinline__ floatx4 dw_tile(const float* A, const float* B, int f
 #pragma unroll 2
   for (int u = 0; u < NROWS / 16; ++u) {
 #pragma unroll
-    for (int v = 0; v < 4; ++v) acc = mfma4(ap[rb[v] + 1024 * u], bp[rb[v] + 1024 * u], acc);
+    for (int v = 0; v < 4; ++v) acc = mfma4(ap[rb[v] + DDRL_LBLK * u], bp[rb[v] + DDRL_LBLK * u], acc);
   }
   return acc;
 }
@@ -459,7 +487,7 @@ __device__ __forceinline__ void dw_tile2(const float* A, const float* B, int fa0
   for (int u = 0; u < NROWS / 16; ++u) {
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const int o = rb[v] + 1024 * u;
+      const int o = rb[v] + DDRL_LBLK * u;
       a0 = mfma4(ap0[o], bp0[o], a0);
       a1 = mfma4(ap1[o], bp1[o], a1);
     }
@@ -482,7 +510,7 @@ __device__ __forceinline__ floatx4 dw_tile_head(const float* A, const float* D, 
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const float bv = cv ? dp[(16 * u + 4 * v) * O] : 0.f;
-      acc = mfma4(ap[rb[v] + 1024 * u], bv, acc);
+      acc = mfma4(ap[rb[v] + DDRL_LBLK * u], bv, acc);
     }
   }
   return acc;

@@ -20,8 +20,9 @@ __host__ __device__ inline FfnOffsets ffn_offsets(int d, int A) {
 }
 
 // LDS image of both branches: [pol w1 48x64][pol w2][val w1][val w2][b1 b2 vb1 vb2][wo][bo][vo][vbo]
-#define LDS_W1 (48 * 64)
-#define LDS_W2 (64 * 64)
+// (w1 / w2: swizzled images of DDRL_LRS floats per row, common.h)
+#define LDS_W1 DDRL_LIMG(48)
+#define LDS_W2 DDRL_LIMG(64)
 __device__ inline void stage_weights(const float* __restrict__ th, int d, int A, float* lds,
                                      NetLds& P, NetLds& V, int nthreads) {
   const FfnOffsets o = ffn_offsets(d, A);

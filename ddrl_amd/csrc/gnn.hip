@@ -108,12 +108,13 @@ __device__ __forceinline__ float quad_prev(float v) { return dpp_mov<0x93>(v); }
 __device__ __forceinline__ float quad_next(float v) { return dpp_mov<0x39>(v); }   // [1,2,3,0]
 
 // LDS (floats): part [4 waves][16][64] (hypernet partials; later dz exchange), h / du / dm
-// images [16][64] swizzled, head partials [4][16][4], per-graph dout [4][4], stats [4][8].
+// images [16][64] swizzled (DDRL_LBLK floats each, common.h), head partials [4][16][4],
+// per-graph dout [4][4], stats [4][8].
 #define L_PART 0
 #define L_H (L_PART + 4096)
-#define L_DU (L_H + 1024)
-#define L_DM (L_DU + 1024)
-#define L_HP (L_DM + 1024)
+#define L_DU (L_H + DDRL_LBLK)
+#define L_DM (L_DU + DDRL_LBLK)
+#define L_HP (L_DM + DDRL_LBLK)
 #define L_DOUT (L_HP + 256)
 #define L_ST (L_DOUT + 16)
 #define L_SEL (L_ST + 32)
@@ -121,9 +122,10 @@ __device__ __forceinline__ float quad_next(float v) { return dpp_mov<0x39>(v); }
 #define L_QT (L_TP + 8 * 1024)    // quaternions of the tile's 16 graph-nodes [16][4]
 #define L_TOTAL (L_QT + 64)
 // inside L_TP (used only by the hypernetwork backward, after every layer tile is done):
-#define L_M (L_TP)                // MPNN2: message image m [16][64] swizzled
-#define L_DMR (L_TP + 1024)       // MPNN2: ring(dm) image
-#define L_GA (L_TP + 2048)        // GAT1: cross-wave partial dots [4 waves][16 nodes][4]
+#define L_M (L_TP)                      // MPNN2: message image m [16][64] swizzled
+#define L_DMR (L_TP + DDRL_LBLK)        // MPNN2: ring(dm) image
+#define L_GA (L_TP + 2 * DDRL_LBLK)     // GAT1: cross-wave partial dots [4 waves][16 nodes][4]
+static_assert(2 * DDRL_LBLK + 256 <= 8 * 1024, "MPNN2 / GAT1 images inside the hypernet-backward tiles");
 
 // Partial-gradient stores: read once, by the reduction kernel, mostly on other XCDs.
 // Nontemporal stores stream them out of the XCD's L2 while the kernel runs instead of
@@ -144,6 +146,13 @@ __device__ __forceinline__ void pst4(bool l2, float* p, floatx4 v) {
   else __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(p));
 }
 __device__ __forceinline__ float leaky02(float x) { return x > 0.f ? x : 0.2f * x; }   // tf.nn.leaky_relu
+
+// Hypernetwork-backward transpose tiles [16 rows][16 columns]: the 4-float chunk q of row c sits
+// at chunk q ^ ((c >> 1) & 3) of its row (round 5), so the rows' ds_write_b128 (8-lane groups) and
+// the transposed ds_read_b32 (lane c reads column c of a row) are both bank-conflict free; the
+// plain [c][4q] layout made the stores 4-way.
+__device__ __forceinline__ int tp_w(int c, int q) { return c * 16 + ((q ^ ((c >> 1) & 3)) << 2); }
+__device__ __forceinline__ int tp_r(int row, int c) { return row * 16 + (c ^ (((row >> 1) & 3) << 2)); }
 
 // Diagnostic build only (-DDDRL_GNN_STAMPS, tools/diag_gnn_stamps.py): s_memrealtime (100 MHz,
 // one clock for the whole chip) at the phase boundaries of the gradient launch, thread 0 of the
@@ -754,7 +763,7 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds, const in
         const float wn = tanh_fast(pre[r]);
         dp[r] = fi[k] * dz[t][r] * (1.f - wn * wn);
       }
-      *reinterpret_cast<floatx4*>(tp + 256 * t + c * 16 + 4 * q) = dp;   // [row c][j 4q + r]
+      *reinterpret_cast<floatx4*>(tp + 256 * t + tp_w(c, q)) = dp;   // [row c][j 4q + r]
     }
   };
   constexpr int NK = (GF + 3) / 4;   // feature rows of wave 0 (waves 1..3 have NK or NK - 1)
@@ -778,14 +787,14 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds, const in
           const float wn = tanh_fast(pre[r]);
           dp[r] = fi[k] * dz[t][r] * (1.f - wn * wn);
         }
-        *reinterpret_cast<floatx4*>(tpb + 256 * t + c * 16 + 4 * q) = dp;
+        *reinterpret_cast<floatx4*>(tpb + 256 * t + tp_w(c, q)) = dp;
       }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         if (gnn_hbwd_owner(k, t) != zs) continue;
         floatx4 acc = splat4(0.f);
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) acc = mfma4(tpb[256 * t + (4 * s4 + q) * 16 + c], qb[s4], acc);
+        for (int s4 = 0; s4 < 4; ++s4) acc = mfma4(tpb[256 * t + tp_r(4 * s4 + q, c)], qb[s4], acc);
         const int j = i * 64 + 16 * t + 4 * q;
         if (c < 4) pst4(coh, P + off.wenc + c * GHE + j, acc);
         else if (c == 4) pst4(coh, P + off.benc + j, acc);
@@ -804,7 +813,7 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds, const in
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
-      for (int t = 0; t < 4; ++t) a[s4][t] = tp[256 * t + (4 * s4 + q) * 16 + c];
+      for (int t = 0; t < 4; ++t) a[s4][t] = tp[256 * t + tp_r(4 * s4 + q, c)];
     if (k + 1 < GNI && i + 4 < GF) dpre_tiles(k + 1, tpb + 1024 * ((k + 1) & 1));
     floatx4 acc[4];
 #pragma unroll
@@ -995,8 +1004,8 @@ __global__ void __launch_bounds__(256) k_gnn_adam(GnnArgs ga, int nred, int n) {
 // combination's partials are all written -- plain stores into the XCD's L2 -- and read on one
 // XCD:
 //   * each workgroup, once its partials and loss statistics are in L2 (s_waitcnt), raises its
-//     arrival flag (flag[32 k + tile] = this launch's tag and the workgroup's XCC id, agent
-//     scope) and records its XCC for the host's placement check;
+//     arrival flag (flags[32 k + tile] = this launch's tag and the workgroup's XCC id) and
+//     records its XCC for the host's placement check;
 //   * tiles r < R_k of combination k are also its reduction blocks: reducer r waits for the 32
 //     flags of its combination (one per thread, sc1 polls: they miss the CU's own L1; a flag of
 //     this launch from another XCD raises the error word, gnn_wait_flag), sums
@@ -1013,16 +1022,26 @@ __global__ void __launch_bounds__(256) k_gnn_adam(GnnArgs ga, int nred, int n) {
 // every partial written through to memory + one arrival counter 22.7 us per step (256 arrivals
 // on one device-scope atomic serialize, MI355X_MICROARCH.md "fanin"), flags 21.5, release /
 // acquire 33.1, against 18.9 for three launches.
-// Placement guard: a flag carries its writer's XCC id (HW_REG_XCC_ID) below the tag, and a
-// reducer accepts a flag of this launch only from its own XCD.  A flag of this launch from
-// another XCD means the combination straddles XCDs, so its partials may still sit in the other
-// XCD's L2: the reducer raises the error word instead of summing them (the host restores its
-// snapshot and the context goes on with three launches).  Flags are stored at agent scope
-// (written through), so a writer on another XCD is seen -- and refused -- at once rather than
-// after the wait's bound.
+// Placement guard: a flag carries its writer's XCC id (HW_REG_XCC_ID)
+// below the tag, and a reducer accepts a flag of this launch only from its own XCD.  A flag of
+// this launch from another XCD means the combination straddles XCDs, so its partials may still
+// sit in the other XCD's L2: the reducer raises the error word instead of summing them (the host
+// restores its snapshot and the context goes on with three launches).  A flag that stays in the
+// other XCD's L2 is never seen, and the wait ends at its bound the same way.  So no stale partial
+// is ever summed, whatever the flag's scope.  The flags are plain (workgroup-scope) stores into
+// the XCD's L2: agent scope (written through, seen across XCDs at once) cost 0.2 us per step at C5
+// (17.76 vs 17.55 us, profiles/r05/gnn_flag_scope_ab.txt); -DDDRL_GNN_FLAG_AGENT=1 builds it.
 #ifndef DDRL_GNN_FLAG_AGENT
-#define DDRL_GNN_FLAG_AGENT 1
+#define DDRL_GNN_FLAG_AGENT 0
 #endif
+// arrival flag of tile t of combination k: the 32 flags of one combination in one 128-B line,
+// which a reducer's 32 polling lanes read with one request (measured against the flags spread
+// over 8 lines, 4 each: 17.65 / 17.66 vs 17.70 / 17.78 us per step at C5, the same box,
+// profiles/r05/gnn_flag_scope_ab.txt)
+#ifndef DDRL_GNN_FLAG_PACKED
+#define DDRL_GNN_FLAG_PACKED 1
+#endif
+__device__ __forceinline__ int gnn_flag_idx(int k, int t) { return DDRL_GNN_FLAG_PACKED ? 32 * k + t : 8 * t + k; }
 __device__ __forceinline__ unsigned gnn_xcc() {
   unsigned x;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
@@ -1076,7 +1095,7 @@ __device__ __forceinline__ void gnn_tail(const GnnArgs& ga, float* lds, int tile
   // arrival flag of tile `tile` of combination k: this launch's tag and this workgroup's XCC;
   // the placement record for the host check (capi.cpp gnn_placement_broken)
   if (tid == 0) {
-    __hip_atomic_store(ga.flags + 32 * k + tile, (ga.tag << 4) | xcc, __ATOMIC_RELAXED,
+    __hip_atomic_store(ga.flags + gnn_flag_idx(k, tile), (ga.tag << 4) | xcc, __ATOMIC_RELAXED,
                        DDRL_GNN_FLAG_AGENT ? __HIP_MEMORY_SCOPE_AGENT : __HIP_MEMORY_SCOPE_WORKGROUP);
     ga.xcc[32 * k + tile] = (int)xcc;
   }
@@ -1101,7 +1120,7 @@ __device__ __forceinline__ void gnn_tail(const GnnArgs& ga, float* lds, int tile
   }
   // the combination's 32 workgroups have arrived (one flag per thread)
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  const bool ok = tid >= ga.ntiles || gnn_wait_flag(ga, ga.flags + 32 * k + tid, xcc, t0);
+  const bool ok = tid >= ga.ntiles || gnn_wait_flag(ga, ga.flags + gnn_flag_idx(k, tid), xcc, t0);
   if (!__syncthreads_and(ok)) return;
   if (stats) {
     if (tid < 5) {   // all 32 loads in flight (all 32 tiles on this path), then summed in tile order

@@ -115,29 +115,29 @@ __device__ __forceinline__ BranchOff branch_off(const FfnOffsets& o, bool pol) {
   return b;
 }
 
-template <int OB>
+template <int OB, bool PAD>
 __device__ void stage_branch(const float* __restrict__ th, int d, const BranchOff& bo, float* lds,
                              NetLds& W, int ncup) {
-  W.w1 = lds; W.w2 = W.w1 + 48 * 64; W.b1 = W.w2 + 64 * 64; W.b2 = W.b1 + 64;
+  W.w1 = lds; W.w2 = W.w1 + lds_img(48, PAD); W.b1 = W.w2 + lds_img(64, PAD); W.b2 = W.b1 + 64;
   W.wo = W.b2 + 64; W.bo = W.wo + 64 * OB; W.cup = W.bo + OB;   // cup: OB <= 4 (A = 2)
   for (int i = threadIdx.x; i < ncup; i += blockDim.x) W.cup[i] = th[bo.cup + i];
   for (int i = threadIdx.x; i < 48 * 64; i += blockDim.x) {
     const int f = i >> 6;
-    W.w1[sidx(f, i & 63)] = f < d ? th[bo.w1 + i] : 0.f;
+    W.w1[sidx<PAD>(f, i & 63)] = f < d ? th[bo.w1 + i] : 0.f;
   }
-  for (int i = threadIdx.x; i < 64 * 64; i += blockDim.x) W.w2[sidx(i >> 6, i & 63)] = th[bo.w2 + i];
+  for (int i = threadIdx.x; i < 64 * 64; i += blockDim.x) W.w2[sidx<PAD>(i >> 6, i & 63)] = th[bo.w2 + i];
   for (int i = threadIdx.x; i < 64; i += blockDim.x) { W.b1[i] = th[bo.b1 + i]; W.b2[i] = th[bo.b2 + i]; }
   for (int i = threadIdx.x; i < 64 * OB; i += blockDim.x) W.wo[i] = th[bo.wo + i];
   for (int i = threadIdx.x; i < OB; i += blockDim.x) W.bo[i] = th[bo.bo + i];
 }
 // The same image with every weight load of a thread issued before the first LDS store (one
 // memory round trip instead of one per loop trip; NT = threads per workgroup, 256 or 512).
-template <int OB, int NT>
+template <int OB, int NT, bool PAD>
 __device__ __forceinline__ void stage_branch_batched(const float* __restrict__ th, int d, const BranchOff& bo,
                                                      float* lds, NetLds& W, int ncup) {
   static_assert((48 * 64) % NT == 0 && (64 * 64) % NT == 0, "staging split");
   constexpr int N1 = 48 * 64 / NT, N2 = 64 * 64 / NT, NS = (64 * OB + OB + 128 + NT - 1) / NT;
-  W.w1 = lds; W.w2 = W.w1 + 48 * 64; W.b1 = W.w2 + 64 * 64; W.b2 = W.b1 + 64;
+  W.w1 = lds; W.w2 = W.w1 + lds_img(48, PAD); W.b1 = W.w2 + lds_img(64, PAD); W.b2 = W.b1 + 64;
   W.wo = W.b2 + 64; W.bo = W.wo + 64 * OB; W.cup = W.bo + OB;
   const int t = threadIdx.x;
   float a1[N1], a2[N2], as[NS];
@@ -162,12 +162,12 @@ __device__ __forceinline__ void stage_branch_batched(const float* __restrict__ t
 #pragma unroll
   for (int k = 0; k < N1; ++k) {
     const int i = t + NT * k;
-    W.w1[sidx(i >> 6, i & 63)] = a1[k];
+    W.w1[sidx<PAD>(i >> 6, i & 63)] = a1[k];
   }
 #pragma unroll
   for (int k = 0; k < N2; ++k) {
     const int i = t + NT * k;
-    W.w2[sidx(i >> 6, i & 63)] = a2[k];
+    W.w2[sidx<PAD>(i >> 6, i & 63)] = a2[k];
   }
 #pragma unroll
   for (int k = 0; k < NS; ++k) {
@@ -179,7 +179,11 @@ __device__ __forceinline__ void stage_branch_batched(const float* __restrict__ t
   }
   if (t < ncup) W.cup[t] = ac;
 }
-#define BRANCH_LDS_FLOATS (48 * 64 + 64 * 64 + 128 + 64 * 16 + 16)   // multiple of 4 floats
+// LDS floats of one branch's weight image (a multiple of 4 floats)
+__host__ __device__ constexpr int branch_lds_floats(bool pad) { return lds_img(48, pad) + lds_img(64, pad) + 128 + 64 * 16 + 16; }
+// the swizzled image layout of an update kernel (common.h): the padded one, except for the A = 8
+// kernel without the row split, whose LDS budget has room only for the compact images
+__host__ __device__ constexpr bool update_pad(int A, int ksp) { return kLdsPad && !(A == 8 && ksp == 1); }
 
 // "Small" parameters owned one per thread: [dWo 64*OB][dbo OB][db1 64][db2 64], then the
 // policy branch's leg-coupling table [4][A] of the "cup" model
@@ -647,6 +651,7 @@ template <int A, int KS1, int OB, bool POL, int NW, int KSP, bool CUP, bool LSBX
 __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBatch& ub, float* lds, int p, int kq) {
   constexpr int ROWS = DDRL_MB / KSP;
   constexpr int NT = Geo<NW, ROWS>::NT, RT = Geo<NW, ROWS>::RT, NS1 = Geo<NW, ROWS>::NS1, NS2 = Geo<NW, ROWS>::NS2;
+  constexpr bool PAD = update_pad(A, KSP);   // layout of the weight images (common.h)
   const UpdateHyper& H = ub.h;
   const int d = U.d;
   const FfnOffsets of = ffn_offsets(d, A);
@@ -680,7 +685,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 #else
   constexpr int DWR = ROWS;
 #endif
-  float* bufA = lds + BRANCH_LDS_FLOATS;    // feature-major [64][LD]: H1, then X
+  float* bufA = lds + branch_lds_floats(PAD);    // feature-major [64][LD]: H1, then X
   float* bufB = bufA + 64 * LD;             // feature-major [64][LD]: dZ2, then dZ1
   float* Pb = bufB + 64 * LD;               // [NW][NSB] per-wave partial small grads
   float* red = Pb + NW * NSB;               // [NW][8] row-stat partials, [64..] scalars
@@ -720,7 +725,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   if (tid < ROWS) idxb[tid] = U.step0 < last && gok ? row_index(U, U.step0, gr, true) : 0;
   __syncthreads();
   if (U.step0 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, inv_cpr_l, idxb, stg, U.R, ub.lds_bytes);
-  stage_branch_batched<OB, NT>(U.theta, d, bo, lds, W, NCUP);
+  stage_branch_batched<OB, NT, PAD>(U.theta, d, bo, lds, W, NCUP);
   if constexpr (HMF) {
     // the head tile results go to wave 0's partial row; the other waves' dWo partials stay 0
     for (int i = tid; i < NW * NSB; i += NT) Pb[i] = 0.f;
@@ -771,7 +776,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   }
   int ebase[4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) ebase[r] = sidx(4 * q + r, 16 * (w & 3) + c);
+  for (int r = 0; r < 4; ++r) ebase[r] = sidx<PAD>(4 * q + r, 16 * (w & 3) + c);
   float b1p = U.beta_pow[0], b2p = U.beta_pow[1];
   const float adv_mean = U.adv_norm[0], adv_den = U.adv_norm[1];
   const float beta = U.kl_coeff;
@@ -798,7 +803,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     // ---- forward + loss + output gradient (two row tiles) ----
     floatx4 h1[RT][4], h2[RT][4], dz[RT][4];
     float out[RT][OB], dout[RT][OB];
-    ffn_fwd_rt<OB, KS1, RT>(W, cur.x, h1, h2, out);
+    ffn_fwd_rt<OB, KS1, RT, PAD>(W, cur.x, h1, h2, out);
     // "cup" (coupling_net_glorot_uniform_init.py:22-30): means scaled by the record's leg row
     float pre[RT][A], cf[RT][A];
     if constexpr (cup) {
@@ -917,7 +922,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     }
     STAMP(3);
 #ifndef DDRL_ABL_NO_L2BWD
-    layer2_bwd_rt<RT>(W, dz, h2);                        // h2 <- dH1
+    layer2_bwd_rt<RT, PAD>(W, dz, h2);                   // h2 <- dH1
 #endif
 #pragma unroll
     for (int t = 0; t < RT; ++t) dtanh_inplace(h2[t], h1[t]);  // h2 = dZ1
@@ -1227,7 +1232,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 
 #ifndef DDRL_ABL_NO_ADAM
     // ---- tf1 Adam on owned parameters (m, v in registers, weights in LDS) ----
-    // element (f = 16 fa + 4q + r, o = 16 fo + c) sits at ebase[r] + 1024 fa in W1 / W2.
+    // element (f = 16 fa + 4q + r, o = 16 fo + c) sits at ebase[r] + lds_blk(PAD) fa in W1 / W2.
     // All owned weights are read first, then updated, then written (no read-after-write
     // ordering between different parameters' LDS words).
     {
@@ -1236,7 +1241,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       for (int i = 0; i < NTS; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          th[i][r] = (i < NS1 ? W.w2 : W.w1)[ebase[r] + 1024 * tfa[i]];
+          th[i][r] = (i < NS1 ? W.w2 : W.w1)[ebase[r] + lds_blk(PAD) * tfa[i]];
 #pragma unroll
       for (int k = 0; k < NSLOT; ++k) {
         const int e = tid + NT * k;
@@ -1278,7 +1283,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
         for (int r = 0; r < 4; ++r) {
           const int f = 16 * tfa[i] + 4 * q + r;
           if (tv[i] && (i < NS1 || f < d))
-            (i < NS1 ? W.w2 : W.w1)[ebase[r] + 1024 * tfa[i]] = th[i][r];
+            (i < NS1 ? W.w2 : W.w1)[ebase[r] + lds_blk(PAD) * tfa[i]] = th[i][r];
         }
 #pragma unroll
       for (int k = 0; k < NSLOT; ++k) {
@@ -1327,9 +1332,9 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   }
   for (int i = tid; i < 48 * 64; i += NT) {
     const int f = i >> 6;
-    if (f < d) U.theta[bo.w1 + i] = W.w1[sidx(f, i & 63)];
+    if (f < d) U.theta[bo.w1 + i] = W.w1[sidx<PAD>(f, i & 63)];
   }
-  for (int i = tid; i < 64 * 64; i += NT) U.theta[bo.w2 + i] = W.w2[sidx(i >> 6, i & 63)];
+  for (int i = tid; i < 64 * 64; i += NT) U.theta[bo.w2 + i] = W.w2[sidx<PAD>(i >> 6, i & 63)];
   if (POL && tid == 0) {
     U.beta_pow[0] = b1p;
     U.beta_pow[1] = b2p;
@@ -1361,7 +1366,7 @@ static size_t update_lds_bytes(int O, int stride, int ksp) {
   const int nsb = 64 * O + O + 128 + ncup_slots(O, true);
   const int nw = waves_for(O / 2, ksp);
   // + the policy head's H2 / dout images of the row split (HMF in update_loop)
-  return (size_t)(BRANCH_LDS_FLOATS + 2 * 64 * (DDRL_MB / ksp + 8) + nw * nsb + 256 +
+  return (size_t)(branch_lds_floats(update_pad(O / 2, ksp)) + 2 * 64 * (DDRL_MB / ksp + 8) + nw * nsb + 256 +
                   (ksp == 2 ? 80 * (DDRL_MB / ksp + 8) : 0) +
                   (DDRL_MB / ksp) * 4 * stg_chunks(stride, O / 2)) * 4;
 }

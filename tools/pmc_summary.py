@@ -1,17 +1,16 @@
 """Per-step HBM traffic, matrix-core busy fraction and effective clock of the update kernels from
-the rocprofv3 PMC passes of tools/profile_r04.sh (earlier rounds: profile_r02.sh / r03.sh, the
-traffic part only).
+the rocprofv3 PMC passes of tools/profile_r05.sh (earlier rounds: profile_r02.sh - r04.sh).
 
-    python tools/pmc_summary.py gpurun_out/prof4 > profiles/r04/pmc_summary.json
+    python tools/pmc_summary.py gpurun_out/prof5 > profiles/r05/pmc_summary.json
 
 Traffic: FETCH_SIZE and WRITE_SIZE come from separate passes (kB per dispatch); FETCH_SIZE is
 doubled per MI355X_MICROARCH.md (gfx950 tallies 128-B requests at 64 B).  Per workload the
 bytes of every update-kernel dispatch are summed and divided by the minibatch steps they cover:
   local: one fused k_update_ffn launch = 10 epochs x 6400 steps x 4 policies (4096 envs)
   c4:    one fused launch = 10 x 25600 steps x 1 policy (SharedDecentral, 4096 envs)
-  c5:    k_gnn<2, 2> per step (round 4: one launch, the reduction and Adam in its tail; the
-         three-launch step adds k_gnn_reduce + k_gnn_adam), + k_gnn_gather per 1024 steps,
-         10 x 800 steps (128 envs)
+  c5:    k_gnn<2, 2> per step (round 4: one launch, the reduction and Adam in its tail),
+         + k_gnn_gather per 1024 steps, one epoch of 12,800 steps (2048 envs)
+  c5_3launch: the same with DDRL_GNN_TAIL=0 (+ k_gnn_reduce + k_gnn_adam per step)
 
 Matrix cores and clock (pass "MFMA": SQ_VALU_MFMA_BUSY_CYCLES, SQ_BUSY_CYCLES, SQ_WAVE_CYCLES,
 GRBM_GUI_ACTIVE with --kernel-trace), per kernel summed over its dispatches:
@@ -46,14 +45,48 @@ WORKLOADS = {
            "workload": "QuantrupedMultiEnv_SharedDecentral, 4096 envs, T=200 (one fused launch: 10 x 25600 steps)",
            "mfma": {"kernel": "void k_update_ffn<2, 5", "active_simds": 16, "flop_per_step": 2 * (2 * (19 * 64 + 64 * 64 + 64 * 4 + 19 * 64 + 64 * 64 + 64) + (64 * 64 + 64 * 4) + (64 * 64 + 64)) * 128},
            "also": ["void k_act_ffn<2, 5"]},
-    "c5": {"kernels": ["void k_gnn<2, 2", "k_gnn_reduce", "k_gnn_adam", "k_gnn_gather"], "steps": 10 * 800,
-           "workload": "QuantrupedMultiEnv_DecentralShared_Graph, 128 envs, T=200 (10 x 800 steps, one launch "
-                       "each -- three with DDRL_GNN_TAIL=0 --, plus one record gather per 1024 steps)",
+    # round 5: the C5 passes run the bench configuration itself (2048 envs, T = 200: 680 MB of
+    # records, so the per-step record gathers read HBM, not the Infinity Cache), one epoch
+    # (bench.py --sgd-iter 1: 12,800 steps; the per-step figures do not depend on the epochs)
+    "c5": {"kernels": ["void k_gnn<2, 2", "k_gnn_reduce", "k_gnn_adam", "k_gnn_gather"], "steps": 12800,
+           "workload": "QuantrupedMultiEnv_DecentralShared_Graph, 2048 envs, T=200 (one epoch: 12,800 one-launch "
+                       "steps, plus one record gather per 1024 steps)",
            # gradient launch: 32 tiles x 2 nets x 4 backward shares x 4 waves; FLOP: bench.py
            # gnn_flops_per_row(2) x 128 rows (the forward counted once, not once per share)
            "mfma": {"kernel": "void k_gnn<2, 2", "active_simds": 1024, "flop_per_step": 764800 * 128},
            "also": ["void k_gnn<2, 0"]},
+    "c5_3launch": {"kernels": ["void k_gnn<2, 2", "k_gnn_reduce", "k_gnn_adam", "k_gnn_gather"], "steps": 12800,
+                   "workload": "the same with DDRL_GNN_TAIL=0: k_gnn<GRAD> + k_gnn_reduce + k_gnn_adam per step",
+                   "mfma": {"kernel": "void k_gnn<2, 2", "active_simds": 1024, "flop_per_step": 764800 * 128},
+                   "also": ["k_gnn_reduce", "k_gnn_adam"]},
 }
+# LDS / issue counters (tools/profile_r05.sh "lds" passes), summed per kernel over its dispatches
+DETAIL = {"local": "void k_update_ffn<2, 9", "c5": "void k_gnn<2, 2"}
+DETAIL_COUNTERS = ["SQ_LDS_BANK_CONFLICT", "SQ_ACTIVE_INST_LDS", "SQ_INSTS_LDS", "SQ_LDS_ADDR_CONFLICT",
+                   "SQ_INSTS_MFMA", "SQ_INSTS_VALU", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_ANY"]
+
+
+def detail(d):
+    """Per-workload sums of the LDS / issue counters, and the bank-conflict cycles per LDS
+    instruction and per active LDS cycle."""
+    out = {}
+    for name, k in DETAIL.items():
+        pdir = os.path.join(d, f"lds_{name}")
+        path = os.path.join(pdir, "run_counter_collection.csv")
+        if not os.path.exists(path):
+            continue
+        res = {"kernel": k}
+        for c in DETAIL_COUNTERS:
+            v, n = counter(path, c, k)
+            if n:
+                res[c] = v
+                res["dispatches"] = n
+        if res.get("SQ_INSTS_LDS"):
+            res["bank_conflict_cycles_per_lds_inst"] = res.get("SQ_LDS_BANK_CONFLICT", 0.0) / res["SQ_INSTS_LDS"]
+        if res.get("SQ_ACTIVE_INST_LDS"):
+            res["bank_conflict_over_active_lds"] = res.get("SQ_LDS_BANK_CONFLICT", 0.0) / res["SQ_ACTIVE_INST_LDS"]
+        out[name] = res
+    return out
 
 
 def _rows(path):
@@ -128,13 +161,15 @@ def main(d):
         if st and st.get("clock_ghz"):
             LONG_CLOCK_GHZ = st["clock_ghz"]
             break
-    out = {"command": "tools/profile_r04.sh: rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | "
+    out = {"command": "tools/profile_r05.sh: rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | "
                       "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE (separate passes, "
                       "--kernel-trace) -- python3 bench.py --steps 1 --warmup 0 ...",
            "gfx950_fetch_correction": GFX950_FETCH_CORRECTION, "workloads": {}}
     for name, w in WORKLOADS.items():
         per = {}
         total = 0.0
+        if not os.path.isdir(os.path.join(d, f"pmc_{name}_FETCH_SIZE")):
+            continue
         for k in w["kernels"]:
             f_kb, nf = counter(os.path.join(d, f"pmc_{name}_FETCH_SIZE", "run_counter_collection.csv"), "FETCH_SIZE", k)
             w_kb, nw = counter(os.path.join(d, f"pmc_{name}_WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE", k)
@@ -156,6 +191,7 @@ def main(d):
             res["mfma"] = st
             res["mfma_other"] = [x for x in (mfma_stats(mdir, k, None) for k in w.get("also", [])) if x]
         out["workloads"][name] = res
+    out["lds_detail"] = detail(d)
     json.dump(out, sys.stdout, indent=1)
     print()
 
