@@ -197,13 +197,11 @@ def _cpu_update(O, cfg, p, batch, rng):
 
 
 def cpu_sample_envs(env, cpu_envs):
-    """Envs of the bounded CPU sample: cpu_envs for one agent per policy, divided by the agents
-    a shared policy trains on (the same rows per iteration), and by 16 for the GraphNet, whose
-    numpy step costs ~20x the fcnet's (about 10-30 s of CPU work either way)."""
+    """Envs of the bounded CPU sample (about 10-30 s of CPU work on the GPU box): cpu_envs for
+    the fcnet envs, cpu_envs / 16 for the GraphNet, whose numpy step costs ~20x the fcnet's."""
     from ddrl_amd.spec import make_cfg
     cfg, _ = make_cfg(env, 1, 1)
-    k = max(sum(1 for j in range(cfg.n_agents) if cfg.agent_policy[j] == p) for p in range(cfg.n_policies))
-    return max(4, cpu_envs // (16 if cfg.model_kind == 1 else k))
+    return max(4, cpu_envs // 16) if cfg.model_kind == 1 else cpu_envs
 
 
 def cpu_baseline(env, n_envs=128, T=200, seed=0, threads=1):
