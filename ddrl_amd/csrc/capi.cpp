@@ -51,6 +51,7 @@ struct Policy {
   float *stats = nullptr, *grad = nullptr;
   double* partials = nullptr;
   int last_steps = 0;
+  size_t stats_steps = 0;   // rows of `stats` (num_sgd_iter * nb; peer mode may grow it)
 };
 }  // namespace
 
@@ -104,6 +105,15 @@ struct ddrl_ctx {
   hipGraphExec_t rg_exec = nullptr;
   hipStream_t cap_stream = nullptr;    // capture only (the caller's stream may be the null stream)
   const void* rg_key[6] = {nullptr};
+  // peer mode (ddrl_ppo_update_peer): the outboxes shared with the peer context, this context's
+  // row half, the launch tags both contexts step in lockstep, the IPC mapping to close, and the
+  // per-rank virtual shuffle ([nb][128] row indices, this rank's rows in half peer_rank)
+  void* peer_gx = nullptr;
+  int peer_rank = -1;
+  unsigned peer_epoch = 0;
+  void* peer_ipc = nullptr;
+  int32_t* peer_vsh = nullptr;
+  size_t peer_vsh_n = 0;
   std::vector<void*> allocs;
 };
 
@@ -243,6 +253,7 @@ int ddrl_ctx_create(const ddrl_cfg* cfg, int device, ddrl_ctx** out) {
          dalloc(c, &P.last_v, P.C) || dalloc(c, &P.adv_norm, 2) ||
          dalloc(c, &P.partials, (size_t)gae_partials_len(P.C)) ||
          dalloc(c, &P.stats, (size_t)g.num_sgd_iter * P.nb * 8);
+    P.stats_steps = (size_t)g.num_sgd_iter * P.nb;
     if (!rc) {
       // beta1^t, beta2^t, then the arrival counter of the multi-workgroup apply kernel (0)
       float bp[4] = {g.adam_beta1, g.adam_beta2, 0.f, 0.f};
@@ -307,6 +318,7 @@ int ddrl_ctx_destroy(ddrl_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)hipDeviceSynchronize();
   if (c->comm) (void)ncclCommDestroy(c->comm);
+  if (c->peer_ipc) (void)hipIpcCloseMemHandle(c->peer_ipc);
   if (c->rg_exec) (void)hipGraphExecDestroy(c->rg_exec);
   if (c->cap_stream) (void)hipStreamDestroy(c->cap_stream);
   for (void* p : c->allocs) (void)hipFree(p);
@@ -433,7 +445,7 @@ static void launch_ffn(ddrl_ctx* c, const UpdateArgs* ua, const UpdateHyper& h, 
   if (c->fail_step >= 0 && !ua->grad_out) (void)hipMemsetD32Async((hipDeviceptr_t)c->err, 1, 1, c->stream);
   (c->xchg_atomic ? launch_update_ffn_atomic : launch_update_ffn)(
       c->stream, ua, h, nrows, inv_n, c->cfg.act_dim, d, stride, c->cfg.leg_coupling, c->xchg, c->gx, ksp, c->err,
-      &c->upd_epoch, c->xcc);
+      &c->upd_epoch, c->xcc, -1);
 }
 
 int ddrl_synchronize(ddrl_ctx* c) {
@@ -961,7 +973,7 @@ int ddrl_ppo_stats_range(ddrl_ctx* c, int pid, size_t first, size_t n_steps, flo
   CHK_CTX(c);
   if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
   if (!host && n_steps) return fail("null stats buffer");
-  const size_t cap = (size_t)c->cfg.num_sgd_iter * c->pol[pid].nb;
+  const size_t cap = c->pol[pid].stats_steps;
   if (first > cap || n_steps > cap - first) return fail("more stats requested than the schedule holds");
   HIPCHK(hipMemcpyAsync(host, c->pol[pid].stats + first * 8, n_steps * 8 * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
@@ -988,7 +1000,7 @@ int ddrl_ppo_grad(ddrl_ctx* c, int pid, const int32_t* rows, int n_rows, float k
   if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
   if (n_rows < 1 || n_rows > 128) return fail("n_rows must be in [1, 128]");
   if (!rows || !grad) return fail("null rows/grad");
-  if (stats_step >= c->cfg.num_sgd_iter * c->pol[pid].nb) return fail("stats_step beyond the stats buffer");
+  if (stats_step >= (int)c->pol[pid].stats_steps) return fail("stats_step beyond the stats buffer");
   UpdateArgs u = make_update(c, pid, rows, c->zero_perm, kl);
   u.nb = 1; u.n_epochs = 1; u.max_steps = 1; u.step0 = 0; u.grad_out = grad;
   c->snap_mask = 0;   // a gradient launch changes no state: the caller's loop keeps its own snapshot
@@ -1050,7 +1062,7 @@ int ddrl_ppo_update_ddp(ddrl_ctx* c, int pid, const int32_t* shuffle, const int3
   if (!c->comm) return fail("no communicator (ddrl_comm_init)");
   if (!shuffle || !perm || E < 1 || nb < 1) return fail("bad schedule");
   if (m < 1 || m > 128) return fail("rows_per_rank must be in [1, 128]");
-  if (nb > c->cfg.num_sgd_iter * c->pol[pid].nb) return fail("more minibatches than the stats buffer holds");
+  if ((size_t)nb > c->pol[pid].stats_steps) return fail("more minibatches than the stats buffer holds");
   Policy& P = c->pol[pid];
   const int steps = E * nb;
   const UpdateHyper h = make_hyper(c, 1);
@@ -1117,6 +1129,113 @@ int ddrl_ppo_update_ddp(ddrl_ctx* c, int pid, const int32_t* shuffle, const int3
   HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(c->stream));   // the error word of every step
   return check_err(c);
+}
+
+static_assert(sizeof(hipIpcMemHandle_t) == DDRL_PEER_HANDLE_BYTES, "IPC handle size");
+
+int ddrl_peer_alloc(ddrl_ctx* c, void** gx_out, void* ipc_handle_out) {
+  CHK_CTX(c);
+  if (!gx_out) return fail("null outbox pointer");
+  HIPCHK(hipSetDevice(c->device));
+  const size_t bytes = gx_bytes(DDRL_MAXP);
+  void* p = nullptr;
+  HIPCHK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained));
+  c->allocs.push_back(p);
+  HIPCHK(hipMemset(p, 0, bytes));
+  if (ipc_handle_out) {
+    hipIpcMemHandle_t h;
+    HIPCHK(hipIpcGetMemHandle(&h, p));
+    std::memcpy(ipc_handle_out, &h, sizeof(h));
+  }
+  *gx_out = p;
+  return 0;
+}
+
+int ddrl_peer_open(ddrl_ctx* c, const void* ipc_handle, void** gx_out) {
+  CHK_CTX(c);
+  if (!ipc_handle || !gx_out) return fail("null IPC handle / outbox pointer");
+  if (c->peer_ipc) return fail("the context already maps a peer's outboxes");
+  HIPCHK(hipSetDevice(c->device));
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, ipc_handle, sizeof(h));
+  void* p = nullptr;
+  HIPCHK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+  c->peer_ipc = p;
+  *gx_out = p;
+  return 0;
+}
+
+// Peer-mode buffers for E epochs of nb minibatch slots of policy pid: the statistics rows (the
+// union batch has twice this rank's minibatches) and the virtual 128-row shuffle.  Growing them
+// frees and allocates, which waits for the whole device -- for a peer context in the same
+// process, whose launch waits for this one's, that is a stall until the 3 s bound -- so
+// ddrl_peer_attach reserves the configured schedule (num_sgd_iter epochs of R / 64 slots) up front.
+static int peer_reserve(ddrl_ctx* c, int pid, size_t E, size_t nb) {
+  Policy& P = c->pol[pid];
+  if (E * nb > P.stats_steps) {
+    HIPCHK(hipStreamSynchronize(c->stream));
+    dfree(c, &P.stats);
+    P.stats_steps = 0;
+    if (dalloc(c, &P.stats, E * nb * 8)) return -1;
+    P.stats_steps = E * nb;
+  }
+  if (c->peer_vsh_n < nb * DDRL_MB) {
+    HIPCHK(hipStreamSynchronize(c->stream));
+    dfree(c, &c->peer_vsh);
+    c->peer_vsh_n = 0;
+    if (dalloc(c, &c->peer_vsh, nb * DDRL_MB)) return -1;
+    c->peer_vsh_n = nb * DDRL_MB;
+  }
+  return 0;
+}
+
+int ddrl_peer_attach(ddrl_ctx* c, void* gx, int rank, int nranks) {
+  CHK_CTX(c);
+  if (!gx) return fail("null outboxes");
+  if (nranks != 2 || rank < 0 || rank > 1) return fail("peer mode splits the minibatch over exactly two ranks");
+  if (c->cfg.model_kind != DDRL_MODEL_FFN) return fail("peer mode is built for fcnet policies");
+  if (c->update_split != 2) return fail("peer mode needs the row split (DDRL_UPDATE_SPLIT=2, the default)");
+  // rank 0 clears the outboxes (no launch of either rank may be in flight: after a failed update
+  // both ranks have synchronized; rank 1 attaches after rank 0); both count launches from here
+  if (rank == 0) HIPCHK(hipMemsetAsync(gx, 0, gx_bytes(DDRL_MAXP), c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  for (int p = 0; p < c->cfg.n_policies; ++p)
+    if (peer_reserve(c, p, (size_t)c->cfg.num_sgd_iter, (size_t)c->pol[p].R / (DDRL_MB / 2))) return -1;
+  c->peer_gx = gx;
+  c->peer_rank = rank;
+  c->peer_epoch = 0;
+  return 0;
+}
+
+int ddrl_ppo_update_peer(ddrl_ctx* c, int pid, const int32_t* shuffle, const int32_t* perm, int E, int nb, float kl,
+                         int max_steps) {
+  CHK_CTX(c);
+  if (!c->peer_gx) return fail("no peer (ddrl_peer_attach)");
+  if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
+  if (!shuffle || !perm || E < 1 || nb < 1) return fail("bad schedule");
+  Policy& P = c->pol[pid];
+  if ((size_t)nb * (DDRL_MB / 2) > (size_t)P.R) return fail("nb x 64 rows exceed this rank's train batch");
+  if (peer_reserve(c, pid, (size_t)E, (size_t)nb)) return -1;   // no-op within the attached schedule
+  // this rank's rows fill half peer_rank of every 128-row block of the shuffle the kernel indexes
+  // (UpdateArgs::shuffle[slot * 128 + row], row half kq = rows 64 kq .. 64 kq + 63)
+  constexpr int H = DDRL_MB / 2;
+  HIPCHK(hipMemcpy2DAsync(c->peer_vsh + H * c->peer_rank, DDRL_MB * sizeof(int32_t), shuffle, H * sizeof(int32_t),
+                          H * sizeof(int32_t), nb, hipMemcpyDeviceToDevice, c->stream));
+  UpdateArgs u = make_update(c, pid, c->peer_vsh, perm, kl);
+  u.nb = nb;
+  u.n_epochs = E;
+  u.max_steps = max_steps;
+  const int total = E * nb;
+  P.last_steps = max_steps >= 0 ? std::min(total, max_steps) : total;
+  c->kl_last[pid] = kl;
+  if (snapshot(c, 1 << pid)) return -1;
+  c->xcc_pending = 0;   // the atomic protocol is valid for any placement
+  UpdateHyper h = make_hyper(c, 1);
+  launch_update_ffn_atomic(c->stream, &u, h, DDRL_MB, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim, P.d,
+                           P.lay.stride, c->cfg.leg_coupling, c->xchg, static_cast<unsigned long long*>(c->peer_gx), 2,
+                           c->err, &c->peer_epoch, c->xcc, c->peer_rank);
+  HIPCHK(hipGetLastError());
+  return 0;
 }
 
 int ddrl_policy_forward(ddrl_ctx* c, int pid, const float* obs, const int32_t* node, int n,

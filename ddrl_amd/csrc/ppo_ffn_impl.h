@@ -68,6 +68,10 @@ struct UpdateBatch {
   int* xcc;              // [grid] XCC id of every block (placement check, capi.cpp)
   unsigned epoch;        // launch counter (12 bits, never 0): high bits of every exchange tag
   unsigned lds_bytes;    // dynamic LDS of the launch (bounds-checked build)
+  // -1: every row half runs here.  0 / 1 (peer mode, ddrl_ppo_update_peer): only that half runs
+  // in this launch -- the other half is the peer context's launch, which exchanges through the
+  // shared outboxes in gx -- and it writes the weights back and the statistics
+  int own_kq;
 };
 
 // Bounds-checked diagnostic build (-DDDRL_BOUNDS, tools/build_diag.py): every staging,
@@ -420,24 +424,27 @@ __device__ __forceinline__ bool xchg_abandon(unsigned long long t0, int* err) {
 //    never see its partner: the 3 s bound raises the error word and the host names the
 //    atomic build.  With coh set the stores are sc1 (device-coherent write-through: the ISA
 //    of a relaxed agent-scope atomic store), 0.50 us per hop.
-//  * -DDDRL_XCHG_ATOMIC: every granule access is a relaxed agent-scope 64-bit atomic
-//    (__hip_atomic_load / __hip_atomic_store): defined behaviour under the HIP memory model
-//    for any placement, each 8-byte {value, tag} half its own atomic.  The bounds-checked
+//  * -DDDRL_XCHG_ATOMIC: every granule access is a relaxed 64-bit atomic (__hip_atomic_load /
+//    __hip_atomic_store; system scope since round 5, agent before): defined behaviour under the
+//    HIP memory model for any placement, each 8-byte {value, tag} half its own atomic.  The bounds-checked
 //    diagnostic library is built this way, so the GPU suite runs the update under both.
 #if DDRL_XCHG_IS_ATOMIC
+// System scope (round 5): the peer mode's outboxes live in fine-grained memory a peer GPU writes
+// (ddrl_ppo_update_peer); on one device it orders like agent scope.
+#define DDRL_XCHG_SCOPE __HIP_MEMORY_SCOPE_SYSTEM
 typedef unsigned long long* gx_box_t;
 __device__ __forceinline__ gx_box_t gx_rsrc(unsigned long long* box) { return box; }
 __device__ __forceinline__ void gx_put(gx_box_t r, int j, float v0, float v1, unsigned tag, bool) {
   unsigned long long* g = r + 2 * (j * 256 + (int)threadIdx.x);
-  __hip_atomic_store(g, ((unsigned long long)tag << 32) | __float_as_uint(v0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(g, ((unsigned long long)tag << 32) | __float_as_uint(v0), __ATOMIC_RELAXED, DDRL_XCHG_SCOPE);
   __hip_atomic_store(g + 1, ((unsigned long long)tag << 32) | __float_as_uint(v1), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
+                     DDRL_XCHG_SCOPE);
 }
 __device__ __forceinline__ void xchg_store(unsigned long long* g, unsigned long long v, bool) {
-  __hip_atomic_store(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(g, v, __ATOMIC_RELAXED, DDRL_XCHG_SCOPE);
 }
 __device__ __forceinline__ unsigned long long xchg_load(unsigned long long* g) {
-  return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_load(g, __ATOMIC_RELAXED, DDRL_XCHG_SCOPE);
 }
 template <int NP, typename F>
 __device__ __forceinline__ bool gx_get(gx_box_t r, unsigned tag, float* out, int* err, F&& after_first) {
@@ -449,8 +456,8 @@ __device__ __forceinline__ bool gx_get(gx_box_t r, unsigned tag, float* out, int
   for (;;) {
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-      g[2 * j] = __hip_atomic_load(b + 512 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      g[2 * j + 1] = __hip_atomic_load(b + 512 * j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      g[2 * j] = __hip_atomic_load(b + 512 * j, __ATOMIC_RELAXED, DDRL_XCHG_SCOPE);
+      g[2 * j + 1] = __hip_atomic_load(b + 512 * j + 1, __ATOMIC_RELAXED, DDRL_XCHG_SCOPE);
     }
     if (first) { after_first(); first = false; }
     bool ok = true;
@@ -652,6 +659,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   constexpr int ROWS = DDRL_MB / KSP;
   constexpr int NT = Geo<NW, ROWS>::NT, RT = Geo<NW, ROWS>::RT, NS1 = Geo<NW, ROWS>::NS1, NS2 = Geo<NW, ROWS>::NS2;
   constexpr bool PAD = update_pad(A, KSP);   // layout of the weight images (common.h)
+  const int wkq = ub.own_kq < 0 ? 0 : ub.own_kq;   // the half that writes back and writes the statistics
   const UpdateHyper& H = ub.h;
   const int d = U.d;
   const FfnOffsets of = ffn_offsets(d, A);
@@ -1226,7 +1234,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     };
     // KSP = 1: wave 1, right after the exchange (the per-wave partials red[w * 8 + k] are
     // rewritten by the next step's loss); KSP = 2: after sync #6, off every critical path
-    if (KSP == 1 && U.stats && tid == 64 && kq == 0) stats_out();
+    if (KSP == 1 && U.stats && tid == 64 && kq == wkq) stats_out();
     const float scale = red[81];
     const float c1 = 1.f - H.b1, c2 = 1.f - H.b2;
 
@@ -1300,11 +1308,11 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     __syncthreads();                                     // #6: weights updated, stg / idxb ready
     if (tid < ROWS) nxt = step + 3 < last && gok ? row_index(U, step + 3, gr, true) : 0;
     // red[80..81] / red[96..] hold until the next step's exchanges (after its sync #1)
-    if (KSP == 2 && U.stats && tid == 64 && kq == 0) stats_out();
+    if (KSP == 2 && U.stats && tid == 64 && kq == wkq) stats_out();
     STAMP(13);
   }
   STAMP_DONE;
-  if (U.grad_out || kq != 0) return;   // the row halves hold identical state: one writes it back
+  if (U.grad_out || kq != wkq) return;   // the row halves hold identical state: one writes it back
   // a failed launch (an exchange abandoned anywhere: the error word) leaves theta / m / v /
   // beta powers in HBM as they were; the host restores its snapshot for the rest
   if (__hip_atomic_load(ub.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
@@ -1356,6 +1364,7 @@ __global__ void __launch_bounds__(64 * waves_for(A, KSP)) k_update_ffn(UpdateBat
   }
   if (p >= ub.h.P) return;
   const int j = blockIdx.x >> 3, branch = j / KSP, kq = j - branch * KSP;
+  if (ub.own_kq >= 0 && kq != ub.own_kq) return;   // peer mode: the other half runs on the peer context
   const UpdateArgs U = ub.a[p];
   if (branch) update_loop<A, KS1, 1, false, NW, KSP, false, LSBX>(U, ub, lds, p, kq);
   else update_loop<A, KS1, 2 * A, true, NW, KSP, CUP, LSBX>(U, ub, lds, p, kq);
@@ -1386,7 +1395,7 @@ static void launch_update_t(hipStream_t s, UpdateBatch& ub, int P, int stride, i
 
 void DDRL_FFN_LAUNCH(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n,
                        int A, int d, int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp,
-                       int* err, unsigned* epoch_ctr, int* xcc) {
+                       int* err, unsigned* epoch_ctr, int* xcc, int own_kq) {
   UpdateBatch ub;
   for (int p = 0; p < DDRL_MAXP; ++p) ub.a[p] = p < h.P ? ua[p] : UpdateArgs{};
   ub.h = h;
@@ -1396,6 +1405,7 @@ void DDRL_FFN_LAUNCH(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, 
   ub.gx = gx;
   ub.err = err;
   ub.xcc = xcc;
+  ub.own_kq = own_kq;
   // Every granule tag carries the launch epoch (12 bits, per context). Granules are cleared
   // only when the epoch wraps: between two clears every launch's epoch is larger than that
   // of any granule left in the buffers, so a stale granule can never match.  (A memset per
@@ -1405,7 +1415,10 @@ void DDRL_FFN_LAUNCH(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, 
   // in every launch (one fill per iteration); gradient launches keep the epoch-tagged pairs
   const bool lx = ksp == 2 && ua[0].grad_out == nullptr && DDRL_LX;
   if (ub.epoch == 1) (void)hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * 8 * DDRL_MAXP, s);
-  if (ub.epoch == 1 || (lx && !DDRL_XCHG_IS_ATOMIC)) (void)hipMemsetAsync(gx, 0, gx_bytes(DDRL_MAXP), s);
+  // (peer mode: gx is shared with the peer context's launch, which may be running; it is cleared
+  // when the peers attach, ddrl_peer_attach, and its epoch-tagged pairs need no clear per launch)
+  if (own_kq < 0 && (ub.epoch == 1 || (lx && !DDRL_XCHG_IS_ATOMIC)))
+    (void)hipMemsetAsync(gx, 0, gx_bytes(DDRL_MAXP), s);
   if (cup)   // "cup": one shared leg policy, A = 2, d <= 20 (capi validate)
     launch_update_t<2, 5, true>(s, ub, h.P, stride, ksp, lx);
   else

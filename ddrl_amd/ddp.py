@@ -109,8 +109,8 @@ class HipBackend:
     def apply(self, pid, grad):
         self.ctx.ppo_apply(pid, grad)
 
-    def stats(self, pid, n):
-        return self.ctx.ppo_stats(pid, n)
+    def stats(self, pid, n, first=0):
+        return self.ctx.ppo_stats(pid, n, first)
 
     def snapshot(self, pid):
         """Weights, Adam m / v and beta powers of the policy (restored if the update fails)."""
@@ -142,6 +142,7 @@ class DataParallelLearner:
         self.backend, self.comm, self.pid, self.mode = backend, comm, pid, mode
         self.rows_per_rank = minibatch // comm.world if mode == "split" else minibatch
         self.grad_scale = 1.0 if mode == "split" else 1.0 / comm.world
+        self.stats_first = 0   # the row of the last epoch's first step in the learner statistics
 
     def n_minibatches(self, rows_local):
         """Steps per epoch: every rank must run the same number (the smallest shard wins).
@@ -199,7 +200,8 @@ class DataParallelLearner:
         kl_local = 0.0
         if err is None:
             try:
-                st = self.backend.stats(self.pid, nb)
+                st = (self.backend.stats(self.pid, nb, self.stats_first) if self.stats_first else
+                      self.backend.stats(self.pid, nb))
                 kl_local = float(np.mean(st[:, 3].astype(np.float64)))
             except Exception as e:   # the backend's own error (DdrlError from the C-ABI)
                 err = e
@@ -227,3 +229,70 @@ class NativeDataParallelLearner(DataParallelLearner):
         perms = np.asarray(perms, np.int32)
         self.ctx.ppo_update_ddp(self.pid, shuffle, perms, self.rows_per_rank, kl_coeff, self.grad_scale)
         return self._kl(perms.shape[1])
+
+
+def peer_init(ctx, comm):
+    """Peer mode: rank 0 allocates the shared outboxes (fine-grained device memory) and exports
+    an IPC handle, a torch.distributed broadcast hands it to rank 1, which maps it; both attach.
+    Returns the outbox pointer in this process."""
+    from . import native
+    if comm.world != 2:
+        raise ValueError("peer mode splits the minibatch over exactly two ranks")
+    if comm.rank == 0:
+        gx, h = ctx.peer_alloc(export=True)
+    else:
+        h = bytes(native.PEER_HANDLE_BYTES)
+    t = comm.torch.tensor(list(h), dtype=comm.torch.uint8, device=comm.device)
+    comm.dist.broadcast(t, src=0, group=comm.group)
+    if comm.rank == 1:
+        gx = ctx.peer_open(bytes(t.cpu().tolist()))
+    _peer_arm(ctx, comm, gx)
+    return gx
+
+
+def _peer_arm(ctx, comm, gx):
+    """Rank 0's attach clears the outboxes; rank 1 attaches after it (a collective between)."""
+    if comm.rank == 0:
+        ctx.peer_attach(gx, 0, 2)
+    comm.all_reduce_np(np.zeros(1))
+    if comm.rank == 1:
+        ctx.peer_attach(gx, 1, 2)
+
+
+class PeerLearner(DataParallelLearner):
+    """Two ranks' "split" minibatch SGD as ONE fused update split across them
+    (ddrl_ppo_update_peer): rank r's persistent launch runs row half r of every 128-row minibatch
+    (its own 64 rows) and swaps partial gradients and the global-norm partials with the peer's
+    launch every step through the shared outboxes -- device-initiated stores over xGMI, no
+    collective call per step.  Both ranks then run the same clip + Adam, so their weights stay
+    bit-identical, and equal to one fused update over the union batch whose minibatch b is
+    [rank 0's rows | rank 1's rows] (tests/test_gpu_peer.py).  The launches wait for each other
+    (3 s bound), so both must be enqueued close together: the StandardizeFields all-reduce the
+    trainer runs just before is the rendezvous.  A failure on either rank makes both raise with
+    the state of before the call (the flag exchange of `_kl`), and re-arms the outboxes."""
+
+    def __init__(self, ctx, comm, pid=0, minibatch=128):
+        if minibatch != 128:
+            raise ValueError("peer mode splits the fused update's 128-row minibatch")
+        super().__init__(HipBackend(ctx), comm, pid, minibatch, "split")
+        self.ctx = ctx
+        self.gx = peer_init(ctx, comm)
+
+    def learn(self, shuffle, perms, kl_coeff, grad=None):
+        torch = self.comm.torch
+        perms = np.asarray(perms, np.int32)
+        E, nb = perms.shape
+        self.stats_first = (E - 1) * nb
+        snap = self.backend.snapshot(self.pid)
+        pe = torch.from_numpy(np.ascontiguousarray(perms)).to(shuffle.device)
+        err = None
+        try:
+            self.ctx.ppo_update_peer(self.pid, shuffle, pe, kl_coeff)
+            self.ctx.synchronize()
+        except Exception as e:   # DdrlError: this rank's state is already restored
+            err = e
+        try:
+            return self._kl(nb, err, snap)
+        except Exception:
+            _peer_arm(self.ctx, self.comm, self.gx)
+            raise

@@ -86,6 +86,10 @@ _SIGS = {
     "ddrl_comm_init": ([VP, VP, C.c_int, C.c_int], C.c_int),
     "ddrl_comm_allreduce": ([VP, VP, C.c_size_t], C.c_int),
     "ddrl_ppo_update_ddp": ([VP, C.c_int, VP, VP, C.c_int, C.c_int, C.c_int, f32, f32], C.c_int),
+    "ddrl_peer_alloc": ([VP, C.POINTER(VP), VP], C.c_int),
+    "ddrl_peer_open": ([VP, VP, C.POINTER(VP)], C.c_int),
+    "ddrl_peer_attach": ([VP, VP, C.c_int, C.c_int], C.c_int),
+    "ddrl_ppo_update_peer": ([VP, C.c_int, VP, VP, C.c_int, C.c_int, f32, C.c_int], C.c_int),
     "ddrl_policy_forward": ([VP, C.c_int, VP, VP, C.c_int, VP, VP], C.c_int),
     "ddrl_device_buffers": ([VP, C.c_int, C.POINTER(VP), C.POINTER(VP), C.POINTER(VP), C.POINTER(VP)], C.c_int),
     "ddrl_records_get": ([VP, C.c_int, VP, C.c_size_t], C.c_int),
@@ -127,6 +131,7 @@ def header_symbols(path=HEADER):
 
 ABI_VERSION = 4   # DDRL_ABI_VERSION of include/ddrl_hip.h (ddrl_cfg layout, record layout)
 COMM_ID_BYTES = 128   # DDRL_COMM_ID_BYTES (sizeof ncclUniqueId)
+PEER_HANDLE_BYTES = 64   # DDRL_PEER_HANDLE_BYTES (sizeof hipIpcMemHandle_t)
 
 
 def comm_unique_id():
@@ -392,6 +397,30 @@ class Context:
 
     def comm_allreduce(self, buf_dev):
         _ck(self.lib.ddrl_comm_allreduce(self.h, _ptr(buf_dev), buf_dev.numel()))
+
+    def peer_alloc(self, export=False):
+        """Rank 0: the shared outboxes of peer mode; (device pointer, IPC handle bytes or None)."""
+        p = VP()
+        h = (C.c_uint8 * PEER_HANDLE_BYTES)() if export else None
+        _ck(self.lib.ddrl_peer_alloc(self.h, C.byref(p), h))
+        return p.value, (bytes(h) if export else None)
+
+    def peer_open(self, handle):
+        """Rank 1 in another process: map rank 0's outboxes from its IPC handle."""
+        buf = (C.c_uint8 * PEER_HANDLE_BYTES).from_buffer_copy(bytes(handle))
+        p = VP()
+        _ck(self.lib.ddrl_peer_open(self.h, buf, C.byref(p)))
+        return p.value
+
+    def peer_attach(self, gx_ptr, rank, nranks=2):
+        _ck(self.lib.ddrl_peer_attach(self.h, VP(gx_ptr), rank, nranks))
+
+    def ppo_update_peer(self, pid, shuffle_dev, perm_dev, kl_coeff, max_steps=-1):
+        """One fused update with this rank's 64 rows of every minibatch (ddrl_ppo_update_peer);
+        perm_dev: [n_epochs][nb] device int32, shuffle_dev: this rank's nb * 64 row indices."""
+        E, nb = int(perm_dev.shape[0]), int(perm_dev.shape[1])
+        _ck(self.lib.ddrl_ppo_update_peer(self.h, pid, _ptr(shuffle_dev), _ptr(perm_dev), E, nb, float(kl_coeff),
+                                          max_steps))
 
     def ppo_update_ddp(self, pid, shuffle_dev, perms, rows_per_rank, kl_coeff, grad_scale):
         """The data-parallel minibatch loop in C++ (gradient -> RCCL all-reduce -> Adam per step)."""

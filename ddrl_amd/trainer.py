@@ -130,10 +130,14 @@ class PPOTrainer:
             self.rctx.policy_filter_delta_reset()
             self.sched_rng = np.random.default_rng(seed + 7919)   # the same schedule on every rank
         if self.parallel == "ddp":
-            from .ddp import Comm, DataParallelLearner, HipBackend, NativeDataParallelLearner, native_comm_init
+            from .ddp import (Comm, DataParallelLearner, HipBackend, NativeDataParallelLearner, PeerLearner,
+                              native_comm_init)
             rccl = dist.get_backend() == "nccl"
             self.comm = Comm(self.device if rccl else "cpu")
-            if rccl and c.get("ddp_loop", "native") == "native":
+            if c.get("ddp_loop", "native") == "peer":
+                # extension: the two ranks' update as one fused launch split across them
+                self.learner = PeerLearner(self.ctx, self.comm, 0, self.cfg.sgd_minibatch_size)
+            elif rccl and c.get("ddp_loop", "native") == "native":
                 native_comm_init(self.ctx, self.comm)
                 self.learner = NativeDataParallelLearner(self.ctx, self.comm, 0, self.cfg.sgd_minibatch_size,
                                                          c.get("ddp_mode", "split"))
@@ -211,7 +215,7 @@ class PPOTrainer:
         shuffle, perms = self.learner.schedule(self.sched_rng, R, self.cfg.num_sgd_iter)
         kl = self.learner.learn(torch.from_numpy(shuffle).to(self.device), perms, self.kl_coeff[0], self.grad)
         nb = perms.shape[1]
-        last = self.ctx.ppo_stats(0, nb).astype(np.float64).mean(0)
+        last = self.ctx.ppo_stats(0, nb, self.learner.stats_first).astype(np.float64).mean(0)
         pid = self.policy_ids[0]
         learner = {pid: {"cur_kl_coeff": float(np.float32(self.kl_coeff[0])),
                          "cur_lr": float(np.float32(self.cfg.lr)), "total_loss": last[0],

@@ -262,6 +262,33 @@ int ddrl_comm_allreduce(ddrl_ctx* ctx, float* buf_dev, size_t n);
 int ddrl_ppo_update_ddp(ddrl_ctx* ctx, int pid, const int32_t* shuffle_dev, const int32_t* perm_host,
                         int n_epochs, int nb, int rows_per_rank, float kl_coeff, float grad_scale);
 
+/* Peer mode (round 5): the shared-policy minibatch SGD of two ranks as ONE
+ * fused persistent update split across the ranks' contexts -- the reference's 128-row minibatch
+ * ("split" semantics; train_shared_policy_architecture_on_flat.py:48,79 via RLlib's
+ * TrainTFMultiGPU) with rank r's 64 rows of every minibatch in rank r's fused launch, which swaps
+ * its partial gradients with the peer launch every step through shared outboxes (relaxed
+ * system-scope atomics, no collective, no per-step launch), then runs the same clip + Adam:
+ * both ranks' weights stay bit-identical to each other and to one fused launch over the union
+ * batch.  fcnet models, row split on (the default), two ranks.
+ *   ddrl_peer_alloc: rank 0 allocates the outboxes (fine-grained device memory, cleared) and,
+ *     with ipc_handle_out, exports them (DDRL_PEER_HANDLE_BYTES, hipIpcGetMemHandle);
+ *   ddrl_peer_open: rank 1 maps rank 0's outboxes from that handle (another process);
+ *   ddrl_peer_attach: both ranks, before their first peer update (a context in the same
+ *     process passes rank 0's pointer directly); resets the launch tags; rank 0's attach also
+ *     clears the outboxes, so rank 1 attaches after it (and after a failed update both re-attach);
+ *     it reserves the buffers of num_sgd_iter epochs of R / 64 slots (a larger schedule grows
+ *     them, which waits for the whole device: a stall for a peer context of the same process);
+ *   ddrl_ppo_update_peer: shuffle_dev = this rank's nb * 64 row indices (minibatch slot b owns
+ *     entries [64 b, 64 b + 64)), perm_dev[n_epochs][nb] = the slots, the same on both ranks.
+ *     Both ranks must issue the same sequence of peer updates, and each launch needs its peer's
+ *     launch to run concurrently (a wait abandoned after 3 s raises, with the snapshot restored). */
+#define DDRL_PEER_HANDLE_BYTES 64
+int ddrl_peer_alloc(ddrl_ctx* ctx, void** gx_out, void* ipc_handle_out);
+int ddrl_peer_open(ddrl_ctx* ctx, const void* ipc_handle, void** gx_out);
+int ddrl_peer_attach(ddrl_ctx* ctx, void* gx, int rank, int nranks);
+int ddrl_ppo_update_peer(ddrl_ctx* ctx, int pid, const int32_t* shuffle_dev, const int32_t* perm_dev,
+                         int n_epochs, int nb, float kl_coeff, int max_steps);
+
 /* Model forward (ModelV2.forward + value_function) on arbitrary rows:
  * obs_dev[n][d] (ffn; + node_dev[n] = leg index with leg_coupling) or X_dev[n][4][23] +
  * node_dev[n] (gnn). */

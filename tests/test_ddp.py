@@ -204,7 +204,7 @@ class _RecordingCtx:
     def ppo_update_ddp(self, pid, shuffle, perms, m, kl, gscale):
         self.calls.append((pid, shuffle, perms, m, kl, gscale))
 
-    def ppo_stats(self, pid, n):
+    def ppo_stats(self, pid, n, first=0):
         st = np.zeros((n, 8), np.float32)
         st[:, 3] = self.kl_rows[:n]
         return st
