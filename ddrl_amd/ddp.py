@@ -262,29 +262,35 @@ def _peer_arm(ctx, comm, gx):
 class PeerLearner(DataParallelLearner):
     """Two ranks' "split" minibatch SGD as ONE fused update split across them
     (ddrl_ppo_update_peer): rank r's persistent launch runs row half r of every 128-row minibatch
-    (its own 64 rows) and swaps partial gradients and the global-norm partials with the peer's
-    launch every step through the shared outboxes -- device-initiated stores over xGMI, no
-    collective call per step.  Both ranks then run the same clip + Adam, so their weights stay
+    (its own 64 rows) and swaps partial gradients with the peer's launch every step through the
+    shared outboxes -- device-initiated stores (xGMI between GPUs), no collective call and no
+    launch per step.  Both ranks then run the same clip + Adam, so their weights stay
     bit-identical, and equal to one fused update over the union batch whose minibatch b is
     [rank 0's rows | rank 1's rows] (tests/test_gpu_peer.py).  The launches wait for each other
-    (3 s bound), so both must be enqueued close together: the StandardizeFields all-reduce the
-    trainer runs just before is the rendezvous.  A failure on either rank makes both raise with
-    the state of before the call (the flag exchange of `_kl`), and re-arms the outboxes."""
+    (3 s bound), so both must be enqueued close together: the StandardizeFields all-reduce and
+    the minibatch-count all-reduce the trainer runs just before are the rendezvous.
+    A failure on either rank (a wait abandoned at the bound, a refused launch) makes both ranks
+    see it (the flag exchange of `_kl`) with the state of before the call restored; both then
+    fall back to the per-step all-reduce learner (DataParallelLearner over `comm`), this update
+    included, for the rest of the run.  `backend` defaults to the context (HipBackend)."""
 
-    def __init__(self, ctx, comm, pid=0, minibatch=128):
+    def __init__(self, ctx, comm, pid=0, minibatch=128, backend=None):
         if minibatch != 128:
             raise ValueError("peer mode splits the fused update's 128-row minibatch")
-        super().__init__(HipBackend(ctx), comm, pid, minibatch, "split")
+        super().__init__(backend if backend is not None else HipBackend(ctx), comm, pid, minibatch, "split")
         self.ctx = ctx
+        self.fallback = None
         self.gx = peer_init(ctx, comm)
 
     def learn(self, shuffle, perms, kl_coeff, grad=None):
+        if self.fallback is not None:
+            return self.fallback.learn(shuffle, perms, kl_coeff, grad)
         torch = self.comm.torch
         perms = np.asarray(perms, np.int32)
         E, nb = perms.shape
         self.stats_first = (E - 1) * nb
-        snap = self.backend.snapshot(self.pid)
-        pe = torch.from_numpy(np.ascontiguousarray(perms)).to(shuffle.device)
+        snap = self.backend.snapshot(self.pid) if hasattr(self.backend, "snapshot") else None
+        pe = torch.from_numpy(np.ascontiguousarray(perms)).to(getattr(shuffle, "device", "cpu"))
         err = None
         try:
             self.ctx.ppo_update_peer(self.pid, shuffle, pe, kl_coeff)
@@ -293,6 +299,13 @@ class PeerLearner(DataParallelLearner):
             err = e
         try:
             return self._kl(nb, err, snap)
-        except Exception:
-            _peer_arm(self.ctx, self.comm, self.gx)
-            raise
+        except Exception as e:
+            import warnings
+            warnings.warn(f"peer update failed on rank {self.comm.rank} or its peer ({e}); this update and "
+                          "the following ones run on the per-step all-reduce learner")
+            self.stats_first = 0
+            self.fallback = DataParallelLearner(self.backend, self.comm, self.pid, 128, "split")
+            if grad is None:
+                grad = torch.zeros(int(self.ctx.n_params[self.pid]), dtype=torch.float32,
+                                   device=getattr(shuffle, "device", "cpu"))
+            return self.fallback.learn(shuffle, perms, kl_coeff, grad)

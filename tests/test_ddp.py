@@ -344,3 +344,72 @@ def test_learner_error_raises_on_every_rank_world2(where):
     assert msgs[0][0].startswith("RuntimeError") and "other rank" in msgs[0][0]
     assert msgs[0][1] == msgs[1][1] == "2.0"
     assert msgs[0][2] == msgs[1][2] == str([5.0] * 4)   # weights as before the update
+
+
+class _FakePeerCtx:
+    """Stands in for native.Context in peer mode: the peer launch of `fail_rank` is refused, the
+    other rank's launch then abandons its waits (its synchronize raises), as on the GPU."""
+
+    def __init__(self, rank, fail_rank, n_params):
+        self.rank, self.fail_rank, self.n_params, self.calls = rank, fail_rank, [n_params], []
+
+    def peer_alloc(self, export=False):
+        self.calls.append("alloc")
+        return 4096, bytes(64)
+
+    def peer_open(self, handle):
+        self.calls.append("open")
+        return 8192
+
+    def peer_attach(self, gx, rank, nranks=2):
+        self.calls.append(("attach", gx, rank))
+
+    def ppo_update_peer(self, pid, shuffle, perm, kl, max_steps=-1):
+        from ddrl_amd.native import DdrlError
+        self.calls.append(("update", tuple(perm.shape)))
+        if self.rank == self.fail_rank:
+            raise DdrlError("refused (simulated)")
+
+    def synchronize(self):
+        from ddrl_amd.native import DdrlError
+        raise DdrlError("update kernel: an exchange ... was abandoned (simulated)")
+
+
+def _peer_fallback_worker(rank, world, port, out_dir, rows_local, epochs):
+    import torch
+    import torch.distributed as dist
+    from ddrl_amd.ddp import Comm, PeerLearner
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    params = O.ffn_init(np.random.default_rng(7), D, 2 * A)
+    shapes = O.ffn_param_shapes(D, 2 * A)
+    be = OracleBackend(params, shapes, _rank_batch(rank, rows_local), cap=1024)
+    ctx = _FakePeerCtx(rank, 1, be.theta.size)
+    learner = PeerLearner(ctx, Comm("cpu"), 0, MB, backend=be)
+    shuffle, perms = learner.schedule(np.random.default_rng(300 + rank), rows_local, epochs)
+    with pytest.warns(UserWarning, match="per-step all-reduce"):
+        kl = learner.learn(shuffle, perms, 0.2, torch.zeros(be.theta.size))
+    assert learner.fallback is not None and learner.stats_first == 0
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), theta=be.theta, shuffle=shuffle, perms=perms, kl=kl,
+             calls=np.array([str(c) for c in ctx.calls]))
+    dist.destroy_process_group()
+
+
+def test_peer_learner_falls_back_to_allreduce_loop_world2():
+    """PeerLearner over gloo with a stand-in context: rank 0 allocates and attaches before rank 1
+    opens the handle and attaches; a refused peer launch on rank 1 (rank 0's waits abandoned)
+    makes BOTH ranks fall back to the per-step all-reduce learner for the same update, which
+    then matches the single-process union reference like test_ddp_learner_world2[split]."""
+    import torch.multiprocessing as mp
+    rows_local, epochs = 512, 2
+    out = tempfile.mkdtemp()
+    mp.spawn(_peer_fallback_worker, args=(2, _free_port(), out, rows_local, epochs), nprocs=2, join=True)
+    res = [dict(np.load(os.path.join(out, f"r{r}.npz"))) for r in range(2)]
+    assert list(res[0]["calls"][:2]) == ["alloc", "('attach', 4096, 0)"]
+    assert list(res[1]["calls"][:2]) == ["open", "('attach', 8192, 1)"]
+    assert res[0]["calls"][2] == res[1]["calls"][2] == "('update', (2, 8))"
+    np.testing.assert_array_equal(res[0]["theta"], res[1]["theta"])
+    ref, kl_ref = _reference(res, "split", rows_local, epochs)
+    _params_close(res[0]["theta"], ref, res[0]["perms"].size)
+    np.testing.assert_allclose(res[0]["kl"], kl_ref, rtol=1e-5)
