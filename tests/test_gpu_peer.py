@@ -199,3 +199,29 @@ def test_peer_learner_two_processes_match_data_parallel_learner():
         assert frac >= 0.999 and diff.max() <= 2 * 3e-4 * 8 + 1e-5
         np.testing.assert_allclose(a[f"peer_kl{it}"], a[f"python_kl{it}"], rtol=1e-3, atol=1e-7)
     assert not np.array_equal(a["peer_w1"], a["peer_w0"])
+
+
+def test_peer_mode_argument_checks(setup):
+    """The C-ABI refuses what peer mode does not support, before anything is launched."""
+    import torch
+    from ddrl_amd.native import DdrlError
+    S = setup
+    ctx = S["ranks"][0][0]
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+    fresh, _, _ = make_ctx(ENV, N_ENVS, T)
+    try:
+        with pytest.raises(DdrlError, match="no peer"):
+            fresh.ppo_update_peer(0, dev(S["sh"][0]), dev(S["pe"]), 0.2)
+        gx, _ = ctx.peer_alloc()
+        with pytest.raises(DdrlError, match="exactly two ranks"):
+            fresh.peer_attach(gx, 0, 3)
+        with pytest.raises(DdrlError, match="exactly two ranks"):
+            fresh.peer_attach(gx, 2, 2)
+        fresh.peer_attach(gx, 0, 2)
+        too_many = np.zeros((10, S["nb"] + 1), np.int32)
+        with pytest.raises(DdrlError, match="exceed this rank's train batch"):
+            fresh.ppo_update_peer(0, dev(np.zeros(64 * (S["nb"] + 1), np.int32)), dev(too_many), 0.2)
+        with pytest.raises(DdrlError, match="bad policy id"):
+            fresh.ppo_update_peer(1, dev(S["sh"][0]), dev(S["pe"]), 0.2)
+    finally:
+        fresh.close()
