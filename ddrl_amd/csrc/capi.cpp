@@ -111,6 +111,7 @@ struct ddrl_ctx {
   void* peer_gx = nullptr;
   int peer_rank = -1;
   unsigned peer_epoch = 0;
+  unsigned peer_steps = 0;   // steps the attached pair has run (the quads' tag bit and outbox parity)
   void* peer_ipc = nullptr;
   int32_t* peer_vsh = nullptr;
   size_t peer_vsh_n = 0;
@@ -445,7 +446,7 @@ static void launch_ffn(ddrl_ctx* c, const UpdateArgs* ua, const UpdateHyper& h, 
   if (c->fail_step >= 0 && !ua->grad_out) (void)hipMemsetD32Async((hipDeviceptr_t)c->err, 1, 1, c->stream);
   (c->xchg_atomic ? launch_update_ffn_atomic : launch_update_ffn)(
       c->stream, ua, h, nrows, inv_n, c->cfg.act_dim, d, stride, c->cfg.leg_coupling, c->xchg, c->gx, ksp, c->err,
-      &c->upd_epoch, c->xcc, -1);
+      &c->upd_epoch, c->xcc, -1, 0u);
 }
 
 int ddrl_synchronize(ddrl_ctx* c) {
@@ -1204,6 +1205,7 @@ int ddrl_peer_attach(ddrl_ctx* c, void* gx, int rank, int nranks) {
   c->peer_gx = gx;
   c->peer_rank = rank;
   c->peer_epoch = 0;
+  c->peer_steps = 0;
   return 0;
 }
 
@@ -1231,9 +1233,10 @@ int ddrl_ppo_update_peer(ddrl_ctx* c, int pid, const int32_t* shuffle, const int
   if (snapshot(c, 1 << pid)) return -1;
   c->xcc_pending = 0;   // the atomic protocol is valid for any placement
   UpdateHyper h = make_hyper(c, 1);
-  launch_update_ffn_atomic(c->stream, &u, h, DDRL_MB, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim, P.d,
-                           P.lay.stride, c->cfg.leg_coupling, c->xchg, static_cast<unsigned long long*>(c->peer_gx), 2,
-                           c->err, &c->peer_epoch, c->xcc, c->peer_rank);
+  launch_update_ffn_peer(c->stream, &u, h, DDRL_MB, 1.f / c->cfg.sgd_minibatch_size, c->cfg.act_dim, P.d,
+                         P.lay.stride, c->cfg.leg_coupling, c->xchg, static_cast<unsigned long long*>(c->peer_gx), 2,
+                         c->err, &c->peer_epoch, c->xcc, c->peer_rank, c->peer_steps);
+  c->peer_steps += (unsigned)P.last_steps;   // the same count on both ranks
   HIPCHK(hipGetLastError());
   return 0;
 }

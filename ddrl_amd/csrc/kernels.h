@@ -141,15 +141,20 @@ struct UpdateHyper {
 // ksp: 1 = one workgroup per branch, 2 = row split over two (gx: gx_bytes(P) of exchange granules)
 // d / stride: the widest obs width / record stride of the launched policies
 // own_kq: -1 = both row halves in this launch; 0 / 1 = peer mode (that half only; gx shared with
-// the peer context, whose launch runs the other half; atomic protocol only)
+// the peer context, whose launch runs the other half; launch_update_ffn_peer)
+// lx_base: peer mode's global step count before this launch (0 otherwise)
 void launch_update_ffn(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n, int A, int d,
                        int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp, int* err,
-                       unsigned* epoch_ctr, int* xcc, int own_kq = -1);
-// the same with the relaxed system-scope atomic exchange (ppo_ffn_atomic.hip): any placement, and
-// outboxes in memory a peer GPU reads (fine-grained, peer mode)
+                       unsigned* epoch_ctr, int* xcc, int own_kq = -1, unsigned lx_base = 0);
+// the same with the relaxed system-scope atomic exchange (ppo_ffn_atomic.hip): any placement
 void launch_update_ffn_atomic(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n, int A,
                               int d, int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp,
-                              int* err, unsigned* epoch_ctr, int* xcc, int own_kq = -1);
+                              int* err, unsigned* epoch_ctr, int* xcc, int own_kq = -1, unsigned lx_base = 0);
+// peer mode (ppo_ffn_peer.hip): the LSB-tagged quads at system scope, outboxes shared with the
+// peer context's launch (fine-grained memory a peer GPU reads)
+void launch_update_ffn_peer(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n, int A,
+                            int d, int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp,
+                            int* err, unsigned* epoch_ctr, int* xcc, int own_kq = -1, unsigned lx_base = 0);
 // epoch_ctr: per-context launch counter (granule tags)
 size_t gx_bytes(int P);
 // clip_by_global_norm + tf1 Adam on a flat (all-reduced) gradient vector

@@ -7,14 +7,19 @@
 #include "ppo_loss.h"
 
 // One translation unit per exchange protocol: ppo_ffn.hip builds the default (plain stores into
-// the XCD's L2, sc1 polls) as launch_update_ffn, ppo_ffn_atomic.hip the relaxed agent-scope
-// atomic protocol (valid for any workgroup placement) as launch_update_ffn_atomic.  The device
-// code has internal linkage, so the two instantiations of every kernel never meet at link time.
+// the XCD's L2, sc1 polls) as launch_update_ffn, ppo_ffn_atomic.hip the relaxed system-scope
+// atomic protocol (valid for any workgroup placement) as launch_update_ffn_atomic, and
+// ppo_ffn_peer.hip (DDRL_FFN_AT = 2) peer mode's launch_update_ffn_peer: the LSB-tagged quads of
+// the default protocol moved with system-scope buffer accesses (sc0 sc1: written through to
+// memory, read past every cache), whose outboxes a peer context's launch shares.  The device
+// code has internal linkage, so the instantiations of every kernel never meet at link time.
 #ifndef DDRL_FFN_AT
 #define DDRL_FFN_AT 0
 #endif
 
-#if DDRL_FFN_AT
+#if DDRL_FFN_AT == 2
+#define DDRL_FFN_LAUNCH launch_update_ffn_peer
+#elif DDRL_FFN_AT
 #define DDRL_FFN_LAUNCH launch_update_ffn_atomic
 #else
 #define DDRL_FFN_LAUNCH launch_update_ffn
@@ -28,6 +33,10 @@
 #ifndef DDRL_LX
 #define DDRL_LX 1
 #endif
+// the peer TU: atomic granules for the norm exchange and the gradient launches' pairs, quads at
+// system scope for the fused launches' partner exchange
+#define DDRL_XCHG_LXSYS (DDRL_FFN_AT == 2)
+#define DDRL_LX_ON (!DDRL_XCHG_IS_ATOMIC || DDRL_XCHG_LXSYS)
 
 namespace {
 
@@ -72,6 +81,10 @@ struct UpdateBatch {
   // in this launch -- the other half is the peer context's launch, which exchanges through the
   // shared outboxes in gx -- and it writes the weights back and the statistics
   int own_kq;
+  // peer mode: steps the attached pair has run before this launch.  The quads' tag bit and the
+  // outbox parity follow the pair's global step count, so the shared outboxes need no clear
+  // between launches (0 otherwise: the outboxes are cleared before each fused launch)
+  unsigned lx_base;
 };
 
 // Bounds-checked diagnostic build (-DDDRL_BOUNDS, tools/build_diag.py): every staging,
@@ -549,17 +562,31 @@ __device__ __forceinline__ bool gx_get(gx_box_t r, unsigned tag, float* out, int
 // launch) keep the epoch-tagged pairs, which need no clear per launch.
 __device__ __forceinline__ unsigned lx_bit(int step) { return ((unsigned)(step >> 1) & 1u) ^ 1u; }
 __device__ __forceinline__ float lx_t(float v, unsigned bit) { return __uint_as_float((__float_as_uint(v) & ~1u) | bit); }
-#if !DDRL_XCHG_IS_ATOMIC
-__device__ __forceinline__ void gx_put4(gx_box_t r, int j, float a, float b, float c, float d, unsigned bit) {
+#if DDRL_LX_ON
+#if DDRL_XCHG_LXSYS
+// peer TU: the quads' outboxes as buffer resources, stores and loads at system scope (sc0 sc1)
+typedef __amdgpu_buffer_rsrc_t lx_box_t;
+__device__ __forceinline__ lx_box_t lx_rsrc(unsigned long long* box) {
+  return __builtin_amdgcn_make_buffer_rsrc(box, 0, GX_MAX_PAIRS * 256 * 16, 0x00020000);
+}
+#define DDRL_LX_ST 17
+#define DDRL_LX_LD 17
+#else
+typedef gx_box_t lx_box_t;
+__device__ __forceinline__ lx_box_t lx_rsrc(unsigned long long* box) { return gx_rsrc(box); }
+#define DDRL_LX_ST DDRL_GX_ST
+#define DDRL_LX_LD DDRL_GX_LD
+#endif
+__device__ __forceinline__ void gx_put4(lx_box_t r, int j, float a, float b, float c, float d, unsigned bit) {
   const v4u g = {__float_as_uint(lx_t(a, bit)), __float_as_uint(lx_t(b, bit)), __float_as_uint(lx_t(c, bit)),
                  __float_as_uint(lx_t(d, bit))};
-  __builtin_amdgcn_raw_buffer_store_b128(g, r, (j * 256 + (int)threadIdx.x) * 16, 0, DDRL_GX_ST);
+  __builtin_amdgcn_raw_buffer_store_b128(g, r, (j * 256 + (int)threadIdx.x) * 16, 0, DDRL_LX_ST);
 }
 // NX > 0: the timing-only cost-model build of a four-way split; NX more quads (another outbox,
 // rx) loaded with every poll and returned unchecked
 template <int NQ, int NX = 0, typename F>
-__device__ __forceinline__ bool gx_get4(gx_box_t r, unsigned bit, float* out, int* err, F&& after_first,
-                                        gx_box_t rx = gx_box_t()) {
+__device__ __forceinline__ bool gx_get4(lx_box_t r, unsigned bit, float* out, int* err, F&& after_first,
+                                        lx_box_t rx = lx_box_t()) {
   bool lost = false;
   v4u g[NQ + NX];
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -567,9 +594,9 @@ __device__ __forceinline__ bool gx_get4(gx_box_t r, unsigned bit, float* out, in
   for (;;) {
     xchg_inv_l1();
 #pragma unroll
-    for (int j = 0; j < NQ; ++j) g[j] = __builtin_amdgcn_raw_buffer_load_b128(r, (j * 256 + (int)threadIdx.x) * 16, 0, DDRL_GX_LD);
+    for (int j = 0; j < NQ; ++j) g[j] = __builtin_amdgcn_raw_buffer_load_b128(r, (j * 256 + (int)threadIdx.x) * 16, 0, DDRL_LX_LD);
 #pragma unroll
-    for (int j = 0; j < NX; ++j) g[NQ + j] = __builtin_amdgcn_raw_buffer_load_b128(rx, (j * 256 + (int)threadIdx.x) * 16, 0, DDRL_GX_LD);
+    for (int j = 0; j < NX; ++j) g[NQ + j] = __builtin_amdgcn_raw_buffer_load_b128(rx, (j * 256 + (int)threadIdx.x) * 16, 0, DDRL_LX_LD);
     if (first) { after_first(); first = false; }
     unsigned bad = 0;
 #pragma unroll
@@ -679,7 +706,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   // fused launches (LSBX) sum LSB-replaced partials; the default protocol also exchanges them as
   // LSB-tagged quads (LX: small params + stats, then one quad per owned dW tile), the atomic one
   // keeps its {value, tag} pairs and replaces the bits before the sum -- the same sums
-  constexpr bool LX = LSBX && KSP == 2 && !DDRL_XCHG_IS_ATOMIC;
+  constexpr bool LX = LSBX && KSP == 2 && DDRL_LX_ON;
   constexpr int NQ0 = (NSLOT + 1 + 3) / 4;
   constexpr int NQ = NQ0 + NTS;
   static_assert(!LX || NQ <= GX_MAX_PAIRS, "exchange quads");
@@ -950,10 +977,11 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     __syncthreads();                                     // #1: H1, dZ2, partials visible
     STAMP(5);
     const unsigned gtag = xchg_tag(ub.epoch, step);
-    const unsigned lbit = lx_bit(step);
+    const int gstep = step + (int)ub.lx_base;            // outbox parity and quad tag bit
+    const unsigned lbit = lx_bit(gstep);
     (void)lbit;
     const size_t gx_box = (size_t)GX_MAX_PAIRS * 256 * 2;   // granules per outbox
-    const gx_box_t gx_mine = gx_rsrc(ub.gx + ((gx_branch + kq) * 2 + (step & 1)) * gx_box);
+    const gx_box_t gx_mine = gx_rsrc(ub.gx + ((gx_branch + kq) * 2 + (gstep & 1)) * gx_box);
     float gs[NSLOT];
     float st_own = 0.f;
     // small-parameter partials and this half's loss statistics into the exchange (KSP = 2):
@@ -975,13 +1003,14 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       if (tid < NSTAT)
         for (int i = 0; i < NW; ++i) st_own += red[i * 8 + tid];
       v0[NSLOT] = st_own;
-#if !DDRL_XCHG_IS_ATOMIC
+#if DDRL_LX_ON
       if constexpr (LX) {
+        const lx_box_t lx_mine = lx_rsrc(ub.gx + ((gx_branch + kq) * 2 + (gstep & 1)) * gx_box);
         float w0[4 * NQ0];
 #pragma unroll
         for (int k = 0; k < 4 * NQ0; ++k) w0[k] = k <= NSLOT ? v0[k] : 0.f;
 #pragma unroll
-        for (int j = 0; j < NQ0; ++j) gx_put4(gx_mine, j, w0[4 * j], w0[4 * j + 1], w0[4 * j + 2], w0[4 * j + 3], lbit);
+        for (int j = 0; j < NQ0; ++j) gx_put4(lx_mine, j, w0[4 * j], w0[4 * j + 1], w0[4 * j + 2], w0[4 * j + 3], lbit);
         return;
       }
 #endif
@@ -1007,9 +1036,10 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     if constexpr (KSP == 2) {
 #pragma unroll
       for (int i = 0; i < NS1; ++i) {
-#if !DDRL_XCHG_IS_ATOMIC
+#if DDRL_LX_ON
         if constexpr (LX) {
-          gx_put4(gx_mine, NQ0 + i, gt[i][0], gt[i][1], gt[i][2], gt[i][3], lbit);
+          gx_put4(lx_rsrc(ub.gx + ((gx_branch + kq) * 2 + (gstep & 1)) * gx_box), NQ0 + i, gt[i][0], gt[i][1], gt[i][2],
+                  gt[i][3], lbit);
           continue;
         }
 #endif
@@ -1067,37 +1097,38 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       // both workgroups hold the same bits)
 #pragma unroll
       for (int i = NS1; i < NTS; ++i) {
-#if !DDRL_XCHG_IS_ATOMIC
+#if DDRL_LX_ON
         if constexpr (LX) {
-          gx_put4(gx_mine, NQ0 + i, gt[i][0], gt[i][1], gt[i][2], gt[i][3], lbit);
+          gx_put4(lx_rsrc(ub.gx + ((gx_branch + kq) * 2 + (gstep & 1)) * gx_box), NQ0 + i, gt[i][0], gt[i][1], gt[i][2],
+                  gt[i][3], lbit);
           continue;
         }
 #endif
         gx_put(gx_mine, NP0 + 2 * i, gt[i][0], gt[i][1], gtag, coh);
         gx_put(gx_mine, NP0 + 2 * i + 1, gt[i][2], gt[i][3], gtag, coh);
       }
-#if !DDRL_XCHG_IS_ATOMIC
+#if DDRL_LX_ON
       if constexpr (LX) {
 #ifdef DDRL_ABL_XCHG3P
         // timing-only cost-model build: three partners' outboxes polled at once, every load of
         // the three in flight together, and their sum (here the partner's outbox, checked, and
         // 2 NQ quads of its other-parity outbox, unchecked)
         float o4[12 * NQ];
-        gx_get4<NQ, 2 * NQ>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), lbit, o4, ub.err, [&] {
+        gx_get4<NQ, 2 * NQ>(lx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (gstep & 1)) * gx_box), lbit, o4, ub.err, [&] {
           if (step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, inv_cpr_l, idxb, stg, U.R, ub.lds_bytes);
-        }, gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + ((step + 1) & 1)) * gx_box));
+        }, lx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + ((gstep + 1) & 1)) * gx_box));
 #pragma unroll
         for (int k = 0; k < 4 * NQ; ++k) o4[k] = (o4[k] + o4[4 * NQ + k]) + o4[8 * NQ + k];
 #else
         float o4[4 * NQ];
-        gx_get4<NQ>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), lbit, o4, ub.err, [&] {
+        gx_get4<NQ>(lx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (gstep & 1)) * gx_box), lbit, o4, ub.err, [&] {
           if (step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, inv_cpr_l, idxb, stg, U.R, ub.lds_bytes);
         });
 #endif
 #if defined(DDRL_ABL_XCHG3)
         for (int extra = 0; extra < 2; ++extra) {   // the cost-model build, as below
           float o2[4 * NQ];
-          gx_get4<NQ>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), lbit, o2, ub.err, [] {});
+          gx_get4<NQ>(lx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (gstep & 1)) * gx_box), lbit, o2, ub.err, [] {});
 #pragma unroll
           for (int k = 0; k < 4 * NQ; ++k) o4[k] += 0.f * o2[k];
         }
@@ -1118,18 +1149,18 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       // the next step's record gathers go out right behind the first poll's loads (which
       // retire first: vmcnt is in order; a re-poll then waits for them too): 13.0 -> 12.9 us
       // per step against issuing them after the exchange
-      gx_get<NP>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), gtag, o, ub.err, [&] {
+      gx_get<NP>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (gstep & 1)) * gx_box), gtag, o, ub.err, [&] {
         if (step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, inv_cpr_l, idxb, stg, U.R, ub.lds_bytes);
       });
 #else
-      gx_get<NP>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), gtag, o, ub.err, [] {});
+      gx_get<NP>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (gstep & 1)) * gx_box), gtag, o, ub.err, [] {});
 #endif
 #ifdef DDRL_ABL_XCHG3
       // timing-only cost-model build: the two more partner reads of a four-way row split, one
       // after the other (each a poll of the partner's outbox and the transfer of its partials)
       for (int extra = 0; extra < 2; ++extra) {
         float o2[2 * NP];
-        gx_get<NP>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (step & 1)) * gx_box), gtag, o2, ub.err, [] {});
+        gx_get<NP>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (gstep & 1)) * gx_box), gtag, o2, ub.err, [] {});
 #pragma unroll
         for (int k = 0; k < 2 * NP; ++k) o[k] += 0.f * o2[k];
       }
@@ -1395,7 +1426,7 @@ static void launch_update_t(hipStream_t s, UpdateBatch& ub, int P, int stride, i
 
 void DDRL_FFN_LAUNCH(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n,
                        int A, int d, int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp,
-                       int* err, unsigned* epoch_ctr, int* xcc, int own_kq) {
+                       int* err, unsigned* epoch_ctr, int* xcc, int own_kq, unsigned lx_base) {
   UpdateBatch ub;
   for (int p = 0; p < DDRL_MAXP; ++p) ub.a[p] = p < h.P ? ua[p] : UpdateArgs{};
   ub.h = h;
@@ -1406,6 +1437,7 @@ void DDRL_FFN_LAUNCH(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, 
   ub.err = err;
   ub.xcc = xcc;
   ub.own_kq = own_kq;
+  ub.lx_base = lx_base;
   // Every granule tag carries the launch epoch (12 bits, per context). Granules are cleared
   // only when the epoch wraps: between two clears every launch's epoch is larger than that
   // of any granule left in the buffers, so a stale granule can never match.  (A memset per
@@ -1416,8 +1448,9 @@ void DDRL_FFN_LAUNCH(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, 
   const bool lx = ksp == 2 && ua[0].grad_out == nullptr && DDRL_LX;
   if (ub.epoch == 1) (void)hipMemsetAsync(xchg, 0, sizeof(unsigned long long) * 8 * DDRL_MAXP, s);
   // (peer mode: gx is shared with the peer context's launch, which may be running; it is cleared
-  // when the peers attach, ddrl_peer_attach, and its epoch-tagged pairs need no clear per launch)
-  if (own_kq < 0 && (ub.epoch == 1 || (lx && !DDRL_XCHG_IS_ATOMIC)))
+  // when the peers attach, ddrl_peer_attach, and the quads' tag bits follow the pair's global
+  // step count, lx_base, so a value left from an earlier launch never matches)
+  if (own_kq < 0 && (ub.epoch == 1 || (lx && DDRL_LX_ON)))
     (void)hipMemsetAsync(gx, 0, gx_bytes(DDRL_MAXP), s);
   if (cup)   // "cup": one shared leg policy, A = 2, d <= 20 (capi validate)
     launch_update_t<2, 5, true>(s, ub, h.P, stride, ksp, lx);

@@ -266,8 +266,9 @@ int ddrl_ppo_update_ddp(ddrl_ctx* ctx, int pid, const int32_t* shuffle_dev, cons
  * fused persistent update split across the ranks' contexts -- the reference's 128-row minibatch
  * ("split" semantics; train_shared_policy_architecture_on_flat.py:48,79 via RLlib's
  * TrainTFMultiGPU) with rank r's 64 rows of every minibatch in rank r's fused launch, which swaps
- * its partial gradients with the peer launch every step through shared outboxes (relaxed
- * system-scope atomics, no collective, no per-step launch), then runs the same clip + Adam:
+ * its partial gradients with the peer launch every step through shared outboxes (LSB-tagged
+ * quads, system-scope stores and loads; no collective, no per-step launch), then runs the same
+ * clip + Adam:
  * both ranks' weights stay bit-identical to each other and to one fused launch over the union
  * batch.  fcnet models, row split on (the default), two ranks.
  *   ddrl_peer_alloc: rank 0 allocates the outboxes (fine-grained device memory, cleared) and,
