@@ -5,15 +5,16 @@ SharedDecentral ("policy_legs" on all four legs,
 quantruped_singleDecentralizedController_environments.py:21-48), "split" semantics: the
 reference's 128-row minibatch, 64 rows from each rank's shard.  Rank r's fused launch runs row
 half r of every minibatch and swaps its partial gradients with the peer launch every step
-through shared outboxes (relaxed system-scope atomics); both then run the same clip + tf1 Adam.
+through shared outboxes (LSB-tagged quads with system-scope stores and loads, ppo_ffn_peer.hip);
+both then run the same clip + tf1 Adam.
 Rehearsed here as two contexts of one process on one GPU, each on its own stream, so the two
 persistent launches run side by side (the pool gives one GPU: the xGMI path is not exercised).
 
 Checks: both ranks' weights, Adam moments, beta powers and learner statistics are bit-identical
 to each other AND to ONE fused launch (ddrl_ppo_update) over the union batch whose minibatch b is
 [rank 0's 64 rows | rank 1's 64 rows] -- the row halves of that launch do exactly the two ranks'
-arithmetic, and the atomic protocol sums the same LSB-replaced partials as the default one.  Two
-consecutive updates keep the ranks' launch tags in lockstep.  A rank whose peer never launches
+arithmetic on the same LSB-replaced partials.  Two consecutive updates keep the ranks' launch
+tags and global step count (the quads' tag bit) in lockstep.  A rank whose peer never launches
 abandons its waits at the 3 s bound: the call raises and its state is restored.  Then the same as
 two processes sharing the GPU (IPC-mapped outboxes): the trainer's PeerLearner ("ddp_loop":
 "peer") against the per-step all-reduce learner.
