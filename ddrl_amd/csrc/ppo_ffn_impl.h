@@ -29,6 +29,11 @@
 #else
 #define DDRL_XCHG_IS_ATOMIC 0
 #endif
+// Per-lane predicates "feature < d" out of the step loop (the inputs of features >= d zeroed
+// instead; -DDDRL_PADZERO=0: the predicates, for A/B)
+#ifndef DDRL_PADZERO
+#define DDRL_PADZERO 1
+#endif
 // LSB-tagged quads for fused launches (round 4; -DDDRL_LX=0: the {value, tag} pairs everywhere)
 #ifndef DDRL_LX
 #define DDRL_LX 1
@@ -284,7 +289,7 @@ __host__ __device__ constexpr int stg_chunks(int stride, int A) { return A == 8 
 // buffer for the last row, whatever that LDS holds -- and 0 x NaN is NaN.
 template <int A, int KS1, bool POL, int RT>
 __device__ __forceinline__ void load_row(const float* stg, int stg_stride, const RecLayout& L, const int* row_l,
-                                         int d, RowData<A, RT>& r) {
+                                         int d, RowData<A, RT>& r, unsigned xlast_bits = 0xffffffffu) {
   const int q = (threadIdx.x & 63) >> 4;
 #ifdef DDRL_BOUNDS
   {
@@ -302,6 +307,9 @@ __device__ __forceinline__ void load_row(const float* stg, int stg_stride, const
 #pragma unroll
     for (int s = 0; s < 12; ++s)   // exact instances (KS1 = ceil(d / 4)) stay inside the record
       r.x[t][s] = (s < KS1 && (KS1 < 12 || 4 * s + q < d)) ? rp[L.obs + 4 * s + q] : 0.f;
+    // exact instances: the last k-step's features >= d (the record's next columns) -> 0 through
+    // a per-lane bit mask (no lane predicate in the step loop), so the dW1 rows >= d are zero
+    if (KS1 < 12) r.x[t][KS1 - 1] = __uint_as_float(__float_as_uint(r.x[t][KS1 - 1]) & xlast_bits);
     if (POL) {
 #pragma unroll
       for (int j = 0; j < A; ++j) r.act[t][j] = rp[L.act + j];
@@ -819,6 +827,8 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   __syncthreads();
 
   RowData<A, RT> cur;
+  // features 4 (KS1 - 1) + q of the last layer-1 k-step: kept below d, zeroed at and above
+  const unsigned xlast_bits = (KS1 < 12 && 4 * (KS1 - 1) + q >= d) ? 0u : 0xffffffffu;
   // records of step0 -> stg (issued above), row indices of step0 + 1 -> idxb, of step0 + 2 -> nxt
   wait_vmcnt0();
   __syncthreads();
@@ -834,7 +844,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     // Adam's step size (tf1: lr sqrt(1 - b2^t) / (1 - b1^t), correctly rounded sqrt and
     // division) early: its latency hides under the forward's MFMAs
     const float alpha = H.lr * sqrtf(1.f - b2p) / (1.f - b1p);
-    load_row<A, KS1, POL, RT>(stg, 4 * cpr_l, U.lay, row_l, d, cur);
+    load_row<A, KS1, POL, RT>(stg, 4 * cpr_l, U.lay, row_l, d, cur, xlast_bits);
     // ---- forward + loss + output gradient (two row tiles) ----
     floatx4 h1[RT][4], h2[RT][4], dz[RT][4];
     float out[RT][OB], dout[RT][OB];
@@ -1202,7 +1212,10 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int f = 16 * tfa[i] + 4 * q + r;
-        if (tv[i] && (i < NS1 || f < d)) ss += gt[i][r] * gt[i][r];
+        // the weights of features >= d: zero gradient (their inputs are zeroed in load_row), so
+        // only the uniform tile predicate remains in the loop (the generic KS1 = 12 instance
+        // zeroes every feature >= d there too)
+        if (tv[i] && (i < NS1 || DDRL_PADZERO || f < d)) ss += gt[i][r] * gt[i][r];
       }
 
     if (U.grad_out) {   // data-parallel mode: export the raw gradient of this branch
@@ -1321,7 +1334,9 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int f = 16 * tfa[i] + 4 * q + r;
-          if (tv[i] && (i < NS1 || f < d))
+          // (rows >= d of the W1 image: their gradient and moments are zero up to the exchange's
+          // tag bits, they meet only zeroed inputs, and the write-back to HBM skips them)
+          if (tv[i] && (i < NS1 || DDRL_PADZERO || f < d))
             (i < NS1 ? W.w2 : W.w1)[ebase[r] + lds_blk(PAD) * tfa[i]] = th[i][r];
         }
 #pragma unroll
