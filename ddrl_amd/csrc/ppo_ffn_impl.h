@@ -29,6 +29,10 @@
 #else
 #define DDRL_XCHG_IS_ATOMIC 0
 #endif
+// Adam's small-parameter slots past nsb aimed at a sink word instead of masked (A/B: -DDDRL_SINK=0)
+#ifndef DDRL_SINK
+#define DDRL_SINK 1
+#endif
 // Per-lane predicates "feature < d" out of the step loop (the inputs of features >= d zeroed
 // instead; -DDDRL_PADZERO=0: the predicates, for A/B)
 #ifndef DDRL_PADZERO
@@ -804,7 +808,10 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   for (int k = 0; k < NSLOT; ++k) {
     const int e = tid + NT * k;
     ms[k] = vs[k] = 0.f;
-    sp_pidx[k] = sp_lds[k] = 0;
+    sp_pidx[k] = 0;
+    // a slot past the small parameters reads and writes a sink word (red[255], unused), so
+    // Adam's small-parameter LDS accesses need no lane predicate in the step loop
+    sp_lds[k] = DDRL_SINK ? (int)(red + 255 - lds) : 0;
     if (e < nsb) {
       int pidx; float* lp;
       small_param<OB>(e, bo, W, pidx, lp);
@@ -1298,7 +1305,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       for (int k = 0; k < NSLOT; ++k) {
         const int e = tid + NT * k;
         ts[k] = 0.f;
-        ts[k] = e < nsb ? lds[sp_lds[k]] : 0.f;
+        ts[k] = (DDRL_SINK || e < nsb) ? lds[sp_lds[k]] : 0.f;
       }
       // two elements per instruction (v_pk_* ops): the same fused operations, element by
       // element, as the scalar form g = gt s; m += (gt s - m) c1; v += (g g - v) c2;
@@ -1342,7 +1349,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 #pragma unroll
       for (int k = 0; k < NSLOT; ++k) {
         const int e = tid + NT * k;
-        if (e < nsb) lds[sp_lds[k]] = ts[k];
+        if (DDRL_SINK || e < nsb) lds[sp_lds[k]] = ts[k];
       }
     }
 #endif
