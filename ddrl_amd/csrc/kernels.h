@@ -150,6 +150,10 @@ void launch_update_ffn(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h
 void launch_update_ffn_atomic(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n, int A,
                               int d, int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp,
                               int* err, unsigned* epoch_ctr, int* xcc, int own_kq = -1, unsigned lx_base = 0);
+// the KSP = 1 (one workgroup per branch) launches of launch_update_ffn (ppo_ffn_k1.hip)
+void launch_update_ffn_k1(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n, int A,
+                          int d, int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp,
+                          int* err, unsigned* epoch_ctr, int* xcc, int own_kq = -1, unsigned lx_base = 0);
 // peer mode (ppo_ffn_peer.hip): the LSB-tagged quads at system scope, outboxes shared with the
 // peer context's launch (fine-grained memory a peer GPU reads)
 void launch_update_ffn_peer(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n, int A,

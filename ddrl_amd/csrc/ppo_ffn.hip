@@ -20,6 +20,7 @@
 //   partner exchange; global-norm clip; tf1 Adam (m / v in the owning lanes' registers, two
 //   elements per packed instruction, weights updated in place in LDS).
 // ppo_ffn_impl.h holds the device code; DESIGN.md section 3 the measurements behind it.
+#define DDRL_FFN_KSP 2   // the KSP = 1 kernels: ppo_ffn_k1.hip
 #include "ppo_ffn_impl.h"
 
 

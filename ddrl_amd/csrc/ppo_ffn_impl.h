@@ -17,7 +17,15 @@
 #define DDRL_FFN_AT 0
 #endif
 
-#if DDRL_FFN_AT == 2
+// Row-split instances of this TU: 0 both (KSP = 1 and 2), 2 only KSP = 2 (ppo_ffn.hip, built with
+// its own scheduling flags; its KSP = 1 launches go to launch_update_ffn_k1), 1 only KSP = 1
+// (ppo_ffn_k1.hip, the default flags: the KSP = 1 kernels spill more under ppo_ffn.hip's)
+#ifndef DDRL_FFN_KSP
+#define DDRL_FFN_KSP 0
+#endif
+#if DDRL_FFN_KSP == 1
+#define DDRL_FFN_LAUNCH launch_update_ffn_k1
+#elif DDRL_FFN_AT == 2
 #define DDRL_FFN_LAUNCH launch_update_ffn_peer
 #elif DDRL_FFN_AT
 #define DDRL_FFN_LAUNCH launch_update_ffn_atomic
@@ -110,12 +118,24 @@ __device__ __forceinline__ bool bchk(bool ok, int k) {
 }
 }  // namespace
 #if !DDRL_FFN_AT
+#if DDRL_FFN_KSP == 2
+extern "C" int ddrl_diag_bounds_k1(unsigned* host, int reset);
+#endif
+#if DDRL_FFN_KSP == 1
+extern "C" int ddrl_diag_bounds_k1(unsigned* host, int reset) {
+#else
 extern "C" int ddrl_diag_bounds(unsigned* host, int reset) {
+#endif
   if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_bounds), sizeof(g_bounds)) != hipSuccess) return -1;
   if (reset) {
     unsigned z[DDRL_NBOUNDS] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_bounds), z, sizeof(z)) != hipSuccess) return -1;
   }
+#if DDRL_FFN_KSP == 2   // the KSP = 1 kernels' counters (ppo_ffn_k1.hip) count too
+  unsigned k1[DDRL_NBOUNDS];
+  if (ddrl_diag_bounds_k1(k1, reset) != 0) return -1;
+  for (int i = 0; i < DDRL_NBOUNDS; ++i) host[i] += k1[i];
+#endif
   return 0;
 }
 #endif
@@ -390,7 +410,7 @@ __device__ unsigned long long g_stamps[32][16];
 #define STAMP(k) do { if (tid == DDRL_STAMP_TID) { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); st_acc[k] += t_ - st_prev; st_prev = t_; } } while (0)
 #define STAMP_DONE do { if (tid == DDRL_STAMP_TID) for (int k_ = 0; k_ < 16; ++k_) g_stamps[blockIdx.x][k_] = st_acc[k_]; } while (0)
 }  // namespace
-#if !DDRL_FFN_AT
+#if !DDRL_FFN_AT && DDRL_FFN_KSP != 1
 extern "C" int ddrl_diag_stamps(unsigned long long* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) == hipSuccess ? 0 : -1;
 }
@@ -809,9 +829,11 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     const int e = tid + NT * k;
     ms[k] = vs[k] = 0.f;
     sp_pidx[k] = 0;
-    // a slot past the small parameters reads and writes a sink word (red[255], unused), so
-    // Adam's small-parameter LDS accesses need no lane predicate in the step loop
-    sp_lds[k] = DDRL_SINK ? (int)(red + 255 - lds) : 0;
+    // a slot past the small parameters reads and writes a sink word (red[127]: red holds
+    // [0, 64) per-wave statistics, [64, 72) norm partials, 80 / 81, [96, 104) the combined
+    // statistics, and idxb from 128 on), so Adam's small-parameter LDS accesses need no lane
+    // predicate in the step loop
+    sp_lds[k] = DDRL_SINK ? (int)(red + 127 - lds) : 0;
     if (e < nsb) {
       int pidx; float* lp;
       small_param<OB>(e, bo, W, pidx, lp);
@@ -1238,7 +1260,10 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
         const int e = tid + NT * k;
         if (e < nsb) U.grad_out[sp_pidx[k]] = gs[k];
       }
-      if (U.stats && tid == 64) write_stats<POL, NSTAT, NW, KSP>(U.stats + (size_t)step * 8, red, inv_rows);
+      if (U.stats) {
+        __syncthreads();   // red[96 ..] (wave 0) / the per-wave red[w * 8 ..] are read by wave 1
+        if (tid == 64) write_stats<POL, NSTAT, NW, KSP>(U.stats + (size_t)step * 8, red, inv_rows);
+      }
       return;
     }
 
@@ -1436,12 +1461,16 @@ static size_t update_lds_bytes(int O, int stride, int ksp) {
 template <int A, int KS1, bool CUP = false>
 static void launch_update_t(hipStream_t s, UpdateBatch& ub, int P, int stride, int ksp, bool lx) {
   ub.lds_bytes = (unsigned)update_lds_bytes(2 * A, stride, ksp);
+#if DDRL_FFN_KSP != 1
   if (ksp == 2 && lx)
     hipLaunchKernelGGL((k_update_ffn<A, KS1, 2, CUP, true>), dim3(24 + P), dim3(64 * waves_for(A, 2)), ub.lds_bytes, s, ub);
   else if (ksp == 2)
     hipLaunchKernelGGL((k_update_ffn<A, KS1, 2, CUP, false>), dim3(24 + P), dim3(64 * waves_for(A, 2)), ub.lds_bytes, s, ub);
-  else
+#endif
+#if DDRL_FFN_KSP != 2
+  if (ksp == 1)
     hipLaunchKernelGGL((k_update_ffn<A, KS1, 1, CUP, false>), dim3(8 + P), dim3(64 * waves_for(A, 1)), ub.lds_bytes, s, ub);
+#endif
 }
 
 }  // namespace
@@ -1449,6 +1478,12 @@ static void launch_update_t(hipStream_t s, UpdateBatch& ub, int P, int stride, i
 void DDRL_FFN_LAUNCH(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n,
                        int A, int d, int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp,
                        int* err, unsigned* epoch_ctr, int* xcc, int own_kq, unsigned lx_base) {
+#if DDRL_FFN_KSP == 2
+  if (ksp == 1) {   // the KSP = 1 kernels live in ppo_ffn_k1.hip
+    launch_update_ffn_k1(s, ua, h, nrows, inv_n, A, d, stride, cup, xchg, gx, ksp, err, epoch_ctr, xcc, own_kq, lx_base);
+    return;
+  }
+#endif
   UpdateBatch ub;
   for (int p = 0; p < DDRL_MAXP; ++p) ub.a[p] = p < h.P ? ua[p] : UpdateArgs{};
   ub.h = h;
