@@ -150,7 +150,7 @@ void launch_update_ffn(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h
 void launch_update_ffn_atomic(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n, int A,
                               int d, int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp,
                               int* err, unsigned* epoch_ctr, int* xcc, int own_kq = -1, unsigned lx_base = 0);
-// the KSP = 1 (one workgroup per branch) launches of launch_update_ffn (ppo_ffn_k1.hip)
+// the launches of launch_update_ffn other than the fused row split: KSP = 1 and gradient export (ppo_ffn_k1.hip)
 void launch_update_ffn_k1(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, int nrows, float inv_n, int A,
                           int d, int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp,
                           int* err, unsigned* epoch_ctr, int* xcc, int own_kq = -1, unsigned lx_base = 0);

@@ -17,9 +17,10 @@
 #define DDRL_FFN_AT 0
 #endif
 
-// Row-split instances of this TU: 0 both (KSP = 1 and 2), 2 only KSP = 2 (ppo_ffn.hip, built with
-// its own scheduling flags; its KSP = 1 launches go to launch_update_ffn_k1), 1 only KSP = 1
-// (ppo_ffn_k1.hip, the default flags: the KSP = 1 kernels spill more under ppo_ffn.hip's)
+// Kernel instances of this TU: 0 all; 2 only the fused row-split kernels (KSP = 2 with the LSB
+// quads: ppo_ffn.hip, built with its own scheduling flags; every other launch goes to
+// launch_update_ffn_k1); 1 the rest -- KSP = 1 and the gradient-export launches (ppo_ffn_k1.hip,
+// default flags: the KSP = 1 kernels spill more under ppo_ffn.hip's)
 #ifndef DDRL_FFN_KSP
 #define DDRL_FFN_KSP 0
 #endif
@@ -1464,10 +1465,10 @@ static void launch_update_t(hipStream_t s, UpdateBatch& ub, int P, int stride, i
 #if DDRL_FFN_KSP != 1
   if (ksp == 2 && lx)
     hipLaunchKernelGGL((k_update_ffn<A, KS1, 2, CUP, true>), dim3(24 + P), dim3(64 * waves_for(A, 2)), ub.lds_bytes, s, ub);
-  else if (ksp == 2)
-    hipLaunchKernelGGL((k_update_ffn<A, KS1, 2, CUP, false>), dim3(24 + P), dim3(64 * waves_for(A, 2)), ub.lds_bytes, s, ub);
 #endif
 #if DDRL_FFN_KSP != 2
+  if (ksp == 2 && !lx)
+    hipLaunchKernelGGL((k_update_ffn<A, KS1, 2, CUP, false>), dim3(24 + P), dim3(64 * waves_for(A, 2)), ub.lds_bytes, s, ub);
   if (ksp == 1)
     hipLaunchKernelGGL((k_update_ffn<A, KS1, 1, CUP, false>), dim3(8 + P), dim3(64 * waves_for(A, 1)), ub.lds_bytes, s, ub);
 #endif
@@ -1479,7 +1480,9 @@ void DDRL_FFN_LAUNCH(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, 
                        int A, int d, int stride, int cup, unsigned long long* xchg, unsigned long long* gx, int ksp,
                        int* err, unsigned* epoch_ctr, int* xcc, int own_kq, unsigned lx_base) {
 #if DDRL_FFN_KSP == 2
-  if (ksp == 1) {   // the KSP = 1 kernels live in ppo_ffn_k1.hip
+  // only the fused row-split kernels (LSB quads) live here; the KSP = 1 kernels and the
+  // gradient-export launches are built in ppo_ffn_k1.hip
+  if (!(ksp == 2 && ua[0].grad_out == nullptr && DDRL_LX)) {
     launch_update_ffn_k1(s, ua, h, nrows, inv_n, A, d, stride, cup, xchg, gx, ksp, err, epoch_ctr, xcc, own_kq, lx_base);
     return;
   }
