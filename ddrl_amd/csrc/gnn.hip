@@ -51,6 +51,10 @@
 #define GNI 5              // feature rows i per wave (ceil(19 / 4))
 
 enum { GNN_ACT = 0, GNN_FWD = 1, GNN_GRAD = 2 };
+// the wave index as a scalar and the wave's own h block loaded directly (A/B: -DDDRL_GNN_HW=0)
+#ifndef DDRL_GNN_HW
+#define DDRL_GNN_HW 1
+#endif
 // Gradient launches split each tile's backward over GNN_Z workgroups (blockIdx.z): all of
 // them run the forward (the backward needs every activation), workgroup z then computes only
 // the hypernetwork feature rows k % GNN_Z == z of each wave and its Wnode / Wmsg tile slots
@@ -194,7 +198,12 @@ extern "C" int ddrl_diag_gnn_stamps(unsigned long long* host, unsigned long long
 template <int A, int MODE, int NET, int L>
 __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds, const int tile, const int zs) {
   constexpr int O = NET ? 1 : 2 * A;
+#if DDRL_GNN_HW
+  const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, q = lane >> 4,
+            w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar index arithmetic
+#else
   const int tid = threadIdx.x, lane = tid & 63, c = lane & 15, q = lane >> 4, w = tid >> 6;
+#endif
   const int g = c >> 2, n = c & 3;
   const int graph = 4 * tile + g;
   const bool gvalid = graph < ga.n_graphs;
@@ -350,6 +359,13 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds, const in
   for (int fb = 0; fb < 4; ++fb)
 #pragma unroll
     for (int r = 0; r < 4; ++r) h[fb][r] = himg[wbase(r) + 16 * fb];
+#if DDRL_GNN_HW
+  // this wave's own block h[w] (the backward's dtanh): read here, not indexed out of h[][] with
+  // the wave index later (a select chain over every block, ~340 instructions)
+  float hw[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) hw[r] = himg[wbase(r) + 16 * w];
+#endif
   GSTAMP(2);
 
   // ---- message-passing layer: output block w of y (lane: node c, features 16 w + 4 q + r) ----
@@ -711,7 +727,11 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds, const in
   GSTAMP(5);
   // the hypernet partials are consumed: reuse PART for the dz exchange [block][r][lane]
 #pragma unroll
+#if DDRL_GNN_HW
+  for (int r = 0; r < 4; ++r) part[(4 * w + r) * 64 + lane] = dh[r] * (1.f - hw[r] * hw[r]);
+#else
   for (int r = 0; r < 4; ++r) part[(4 * w + r) * 64 + lane] = dh[r] * (1.f - h[w][r] * h[w][r]);
+#endif
   // layer weight gradients: 16 tiles of 16x16 per matrix over the 16 rows, 4 per wave and
   // matrix; tile slot k of this wave belongs to this workgroup's share (gnn_tile_owner)
   // (slot k of wave w: tile id w + 4 k -> matrix k / 4, row block k % 4, column block w)
