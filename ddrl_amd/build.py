@@ -23,12 +23,15 @@ FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I", INCLUDE,
          "-Wno-unused-result"]
 
 
-# per-source extra flags of the production build: the row-split update kernels are scheduled
-# with LLVM's iterative ILP strategy (Local 10.66 -> 10.57 us per step,
-# C4 10.01 -> 9.89, the same state bit for bit; the strategy crashes the compiler on gnn.hip and
-# makes the KSP = 1 kernels spill twice as much, so those stay in ppo_ffn_k1.hip without it)
+# per-source extra flags of the production build:
+#  * the fused row-split update kernels are scheduled with LLVM's iterative ILP strategy (Local
+#    10.66 -> 10.57 us per step, C4 10.01 -> 9.89; it crashes the compiler on gnn.hip and makes
+#    the KSP = 1 kernels spill twice as much, so those stay in ppo_ffn_k1.hip without it);
+#  * MFMA results in VGPRs rather than AGPRs (no v_accvgpr_read before every use): Local 10.59
+#    -> 10.41, C4 9.93 -> 9.69, C5 (gnn.hip) 17.2 -> 16.9.  The state is the same bit for bit.
 _ILP = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
-SRC_FLAGS = {"ppo_ffn.hip": _ILP, "ppo_ffn_peer.hip": _ILP}
+_VGPR_MFMA = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
+SRC_FLAGS = {"ppo_ffn.hip": _ILP + _VGPR_MFMA, "ppo_ffn_peer.hip": _ILP + _VGPR_MFMA, "gnn.hip": _VGPR_MFMA}
 
 
 def _sources():
