@@ -13,10 +13,13 @@ QuantrupedMultiEnv_Local configuration (4 independent per-leg fcnet 2x64 policie
 Multi-GPU: 4096 envs are sharded over the ranks (C3: independent policies, no collective);
 each rank is an independent learner on its shard ("replicas"), value = all ranks' env-steps
 divided by the slowest rank's time.  Shared-policy envs (--env QuantrupedMultiEnv_SharedDecentral,
-..._DecentralShared_Graph) train data-parallel over the ranks instead: the library's RCCL loop
-(ddrl_ppo_update_ddp) by default, DDRL_DDP_LOOP=python for the Python loop, --ddp-mode
-split | local (ddrl_amd/ddp.py).  DDRL_FORCE_DDP=1 runs that learner at one rank (under
-torchrun) and DDRL_DIST_BACKEND=gloo rehearses N ranks on one GPU.
+..._DecentralShared_Graph) default to gather mode at N > 1: every rank rolls out its shard, one
+all-gather of the records per iteration, and every rank runs the same fused update over the union
+batch -- the single-GPU algorithm exactly, the fastest exact mode.
+--shared-mode ddp trains data-parallel instead (RCCL all-reduce of the gradient every SGD step):
+the library's RCCL loop (ddrl_ppo_update_ddp) by default, DDRL_DDP_LOOP=python for the Python
+loop, --ddp-mode split | local (ddrl_amd/ddp.py).  DDRL_FORCE_DDP=1 runs that learner at one rank
+(under torchrun) and DDRL_DIST_BACKEND=gloo rehearses N ranks on one GPU.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 4096] [--env NAME] [--no-cpu-baseline]
 """
@@ -286,10 +289,12 @@ def main():
     ap.add_argument("--ddp-mode", default="split", choices=["split", "local"],
                     help="shared-policy envs on N>1 GPUs: per-rank rows per SGD step (see ddrl_amd/ddp.py); "
                          "split (default) = the reference's 128-row minibatch SGD, local = 128 rows per rank")
-    ap.add_argument("--shared-mode", default="ddp", choices=["ddp", "gather"],
-                    help="N>1 GPUs: 'ddp' (shared-policy envs: RCCL all-reduce of the gradient every SGD step, "
-                         "the north-star mode) or 'gather' (any env: records all-gathered once per iteration, "
-                         "every rank runs the same fused update over the union batch; no per-step collective)")
+    ap.add_argument("--shared-mode", default="auto", choices=["auto", "ddp", "gather"],
+                    help="N>1 GPUs: 'gather' (records all-gathered once per iteration, every rank runs the same "
+                         "fused update over the union batch: the single-GPU algorithm exactly, no per-step "
+                         "collective), 'ddp' (shared-policy envs: RCCL all-reduce of the gradient every SGD "
+                         "step) or 'auto' (default): gather for shared-policy envs -- the fastest exact mode "
+                         "(DESIGN.md section 5) -- and replicas for independent-policy envs")
     args = ap.parse_args()
 
     import torch
@@ -332,8 +337,12 @@ def main():
     gnn = cfg.model_kind == N.MODEL_GNN
     # shared-policy envs on several GPUs train data-parallel (identical weights on every
     # rank); independent-policy envs are replicas (own weights per rank)
-    ddp = (world > 1 or force_ddp) and P == 1 and args.shared_mode == "ddp"
-    gather = (world > 1 or force_ddp) and args.shared_mode == "gather"
+    multi = world > 1 or force_ddp
+    mode = args.shared_mode
+    if mode == "auto":   # DDRL_FORCE_DDP names the data-parallel learner itself
+        mode = "ddp" if force_ddp else ("gather" if P == 1 else "replicas")
+    ddp = multi and P == 1 and mode == "ddp"
+    gather = multi and mode == "gather"
     if gather and args.envs % world:
         raise SystemExit("--shared-mode gather needs --envs divisible by the number of ranks")
     rng = np.random.default_rng(1234 if (ddp or gather) else 1234 + rank)
@@ -357,7 +366,7 @@ def main():
             uctx.params_set(p, ctx.params_get(p))
         R = [T * uctx.layout[p]["C"] for p in range(P)]
         nb = [max(1, r // 128) for r in R]
-        from ddrl_amd.ddp import Comm, sync_standardize, standardize_constants
+        from ddrl_amd.ddp import Comm, gather_records, sync_standardize, standardize_constants
         comm = Comm(f"cuda:{local}" if backend == "nccl" else "cpu") if dist is not None else None
     ev_upd = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     upd_ms = []
@@ -419,15 +428,7 @@ def main():
             for p in range(P):
                 sums = ctx.adv_sums_get(p)
                 uctx.adv_norm_set(p, *(sync_standardize(comm, sums) if comm else standardize_constants(sums)))
-                src, dst = ctx.records_tensor(p), uctx.records_tensor(p)
-                if comm is None:
-                    dst.copy_(src)
-                elif comm.device == "cpu":
-                    parts = [torch.empty_like(src, device="cpu") for _ in range(world)]
-                    dist.all_gather(parts, src.cpu())
-                    dst.copy_(torch.cat(parts).to(dst.device))
-                else:
-                    dist.all_gather_into_tensor(dst, src)
+                gather_records(comm, ctx.records_tensor(p), uctx.records_tensor(p))
         # SampleBatch.shuffle + per-epoch minibatch permutations of every policy: one batched
         # argsort of fp64 uniforms each (policies of one env have equal batch sizes)
         if len(set(R)) == 1:
@@ -530,9 +531,10 @@ def main():
     achieved_tf = flops_launch / (upd_avg_ms * 1e-3) / 1e12
     ks1 = (d + 3) // 4
     # the GNN gradient launch reduces over its tiles in its own tail when it covers a full
-    # 128-row minibatch (32 tiles per combination) and DDRL_GNN_TAIL is not 0 (gnn.hip
-    # launch_step_gnn: ga.tail); the fused step then also runs clip + Adam there
-    gnn_tail = os.environ.get("DDRL_GNN_TAIL", "1") != "0" and rows_per_step == 128
+    # 128-row minibatch (32 tiles per combination) and the context runs the one-launch step
+    # (gnn.hip launch_step_gnn: ga.tail) -- asked of the library, which may have turned it off
+    # (DDRL_GNN_TAIL=0, occupancy / owner-list refusal, fallback after a failed step)
+    gnn_tail = gnn and rows_per_step == 128 and (uctx or ctx).gnn_one_launch()
     pkey = pmc_key(args.env, gnn_tail)
     if gnn:
         if ddp:

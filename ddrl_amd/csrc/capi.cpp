@@ -112,6 +112,7 @@ struct ddrl_ctx {
   int peer_rank = -1;
   unsigned peer_epoch = 0;
   unsigned peer_steps = 0;   // steps the attached pair has run (the quads' tag bit and outbox parity)
+  int peer_inflight = 0;     // a peer launch is enqueued and not yet checked (check_err)
   void* peer_ipc = nullptr;
   int32_t* peer_vsh = nullptr;
   size_t peer_vsh_n = 0;
@@ -392,26 +393,47 @@ static int gnn_placement_broken(ddrl_ctx* c) {
   return bad;
 }
 
+// A failed peer launch may have left partly written outboxes on both ranks: the pair must
+// re-attach (rank 0's attach clears them) before another peer update, or a retry's tag bit could
+// admit the aborted launch's stale quads.  Detaching makes ddrl_ppo_update_peer
+// refuse ("no peer") until ddrl_peer_attach runs again.
+static void peer_detach(ddrl_ctx* c) {
+  c->peer_gx = nullptr;
+  c->peer_rank = -1;
+  c->peer_inflight = 0;
+}
+
 static int check_err(ddrl_ctx* c) {
   int e = 0;
   HIPCHK(hipMemcpy(&e, c->err, sizeof(int), hipMemcpyDeviceToHost));
+  const int was_peer = c->peer_inflight;
+  c->peer_inflight = 0;
   if (e) {
     (void)hipMemset(c->err, 0, sizeof(int));
     const int bad = placement_broken(c);
     const int gbad = gnn_placement_broken(c);
     if (restore_snapshot(c)) return -1;
     c->snap_mask = 0;
+    if (was_peer) {
+      peer_detach(c);
+      return fail("peer update: an exchange with the peer rank's launch was abandoned (3 s timeout or a failed "
+                  "launch).  The weights, Adam state and beta powers are as before the call; this context is "
+                  "detached from its peer: both ranks must call ddrl_peer_attach again before a peer update");
+    }
     if (c->cfg.model_kind == DDRL_MODEL_GNN) {
       // a one-launch GNN step whose waits were abandoned or refused a flag from another XCD:
       // the context goes on with the three-launch step (no cross-workgroup waits)
-      const int was_tail = c->gnn.tail;
+      const int was_tail = c->gnn.tail && c->gnn.lists == 1;
       c->gnn.tail = 0;
+      if (!was_tail)   // the three-launch step has no waits between workgroups
+        return fail("GraphNet update: a launch reported an error (the error word was set).  The weights, Adam "
+                    "state and beta powers are as before the call");
       return fail(std::string("GraphNet update: ") +
                   (gbad ? "the workgroups of a (net, backward share) combination ran on different XCDs (placement "
                           "check), so the one-launch step's reduction through the XCD's L2 was refused"
                         : "a wait between workgroups was abandoned (3 s timeout or a failed launch)") +
-                  ".  The weights, Adam state and beta powers are as before the call" +
-                  (was_tail ? "; this context has switched to the three-launch step: call the update again" : ""));
+                  ".  The weights, Adam state and beta powers are as before the call; this context has switched "
+                  "to the three-launch step: call the update again");
     }
     if (bad && !c->xchg_atomic) {
       c->xchg_atomic = 1;
@@ -1237,7 +1259,20 @@ int ddrl_ppo_update_peer(ddrl_ctx* c, int pid, const int32_t* shuffle, const int
                          P.lay.stride, c->cfg.leg_coupling, c->xchg, static_cast<unsigned long long*>(c->peer_gx), 2,
                          c->err, &c->peer_epoch, c->xcc, c->peer_rank, c->peer_steps);
   c->peer_steps += (unsigned)P.last_steps;   // the same count on both ranks
-  HIPCHK(hipGetLastError());
+  c->peer_inflight = 1;
+  const hipError_t le = hipGetLastError();
+  if (le != hipSuccess) {
+    peer_detach(c);
+    return fail(std::string("peer update launch refused: ") + hipGetErrorString(le) +
+                "; this context is detached from its peer (both ranks re-attach)");
+  }
+  return 0;
+}
+
+int ddrl_gnn_one_launch(ddrl_ctx* c, int* on) {
+  CHK_CTX(c);
+  if (!on) return fail("null output");
+  *on = c->cfg.model_kind == DDRL_MODEL_GNN && c->gnn.tail && c->gnn.lists == 1;
   return 0;
 }
 

@@ -97,6 +97,26 @@ def sync_standardize(comm, sums):
     return standardize_constants(comm.all_reduce_np(np.asarray(sums, np.float64)))
 
 
+def gather_records(comm, src, dst):
+    """Gather mode: every rank's record buffer `src` ([rows][stride] fp32, device) into the
+    union buffer `dst` of the learner context, rank-major (rank r's rows at r * rows).  The union
+    is a row permutation of one process's time-major batch over all envs, and the update's
+    shuffle is a random permutation, so the two are the same SGD problem.  `comm` None: one
+    process (a plain copy).  RCCL gathers straight into `dst`; gloo goes through host memory."""
+    if comm is None or comm.world == 1:
+        dst.copy_(src)
+        return
+    if dst.shape[0] != src.shape[0] * comm.world or dst.shape[1:] != src.shape[1:]:
+        raise ValueError(f"union buffer {tuple(dst.shape)} is not {comm.world} x {tuple(src.shape)}")
+    torch = comm.torch
+    if comm.device == "cpu":   # gloo
+        parts = [torch.empty_like(src, device="cpu") for _ in range(comm.world)]
+        comm.dist.all_gather(parts, src.cpu(), group=comm.group)
+        dst.copy_(torch.cat(parts).to(dst.device))
+    else:
+        comm.dist.all_gather_into_tensor(dst, src, group=comm.group)
+
+
 class HipBackend:
     """The C-ABI context as a learner backend."""
 
@@ -238,6 +258,17 @@ def peer_init(ctx, comm):
     from . import native
     if comm.world != 2:
         raise ValueError("peer mode splits the minibatch over exactly two ranks")
+    # which GPU each rank's context is on: every test ran both ranks on one GPU; the cross-GPU
+    # path (system-scope stores over xGMI into the peer's fine-grained HBM, IPC mapping across
+    # devices) has not run on hardware, so it is flagged, and PeerLearner checks the
+    # ranks' weights after every update
+    dev = comm.torch.cuda.current_device() if comm.torch.cuda.is_available() else -1
+    pci = comm.all_gather_np(np.array([dev], np.int64))
+    if len({int(p[0]) for p in pci}) > 1:
+        import warnings
+        warnings.warn("peer mode across two GPUs is experimental: its cross-device exchange has not run on "
+                      "hardware; the ranks' weights are compared after every update and a mismatch falls back "
+                      "to the all-reduce learner")
     if comm.rank == 0:
         gx, h = ctx.peer_alloc(export=True)
     else:
@@ -297,6 +328,21 @@ class PeerLearner(DataParallelLearner):
             self.ctx.synchronize()
         except Exception as e:   # DdrlError: this rank's state is already restored
             err = e
+        # both ranks must hold bit-identical weights after a completed peer update; a mismatch (a
+        # partial the peer never saw) is a failure like an abandoned exchange: both restore the
+        # snapshot and fall back
+        digest = np.zeros(2)
+        if err is None:
+            theta = np.asarray(self.ctx.params_get(self.pid))
+            digest = np.array([float(np.sum(theta, dtype=np.float64)),
+                               float(np.dot(theta.astype(np.float64), np.arange(1, theta.size + 1)))])
+        both = self.comm.all_gather_np(digest)
+        if err is None and not np.array_equal(both[0], both[1]) and np.all(np.isfinite(both)):
+            if not any(np.all(b == 0) for b in both):   # the other rank failed: its error wins below
+                err = RuntimeError("peer update: the two ranks' weights differ after the fused update (the peer's "
+                                   "partials were not seen); the state of before the call is restored")
+                if snap is not None:
+                    self.backend.restore(self.pid, snap)
         try:
             return self._kl(nb, err, snap)
         except Exception as e:

@@ -91,6 +91,7 @@ _SIGS = {
     "ddrl_peer_attach": ([VP, VP, C.c_int, C.c_int], C.c_int),
     "ddrl_ppo_update_peer": ([VP, C.c_int, VP, VP, C.c_int, C.c_int, f32, C.c_int], C.c_int),
     "ddrl_policy_forward": ([VP, C.c_int, VP, VP, C.c_int, VP, VP], C.c_int),
+    "ddrl_gnn_one_launch": ([VP, C.POINTER(C.c_int)], C.c_int),
     "ddrl_device_buffers": ([VP, C.c_int, C.POINTER(VP), C.POINTER(VP), C.POINTER(VP), C.POINTER(VP)], C.c_int),
     "ddrl_records_get": ([VP, C.c_int, VP, C.c_size_t], C.c_int),
     "ddrl_records_set": ([VP, C.c_int, VP, C.c_size_t], C.c_int),
@@ -421,6 +422,13 @@ class Context:
         E, nb = int(perm_dev.shape[0]), int(perm_dev.shape[1])
         _ck(self.lib.ddrl_ppo_update_peer(self.h, pid, _ptr(shuffle_dev), _ptr(perm_dev), E, nb, float(kl_coeff),
                                           max_steps))
+
+    def gnn_one_launch(self):
+        """True when the GraphNet minibatch step runs as one launch (reduction + clip + Adam in
+        the gradient launch's tail), False for the three-launch step or an fcnet context."""
+        on = C.c_int()
+        _ck(self.lib.ddrl_gnn_one_launch(self.h, C.byref(on)))
+        return bool(on.value)
 
     def ppo_update_ddp(self, pid, shuffle_dev, perms, rows_per_rank, kl_coeff, grad_scale):
         """The data-parallel minibatch loop in C++ (gradient -> RCCL all-reduce -> Adam per step)."""

@@ -134,10 +134,24 @@ class PPOTrainer:
                               native_comm_init)
             rccl = dist.get_backend() == "nccl"
             self.comm = Comm(self.device if rccl else "cpu")
-            if c.get("ddp_loop", "native") == "peer":
-                # extension: the two ranks' update as one fused launch split across them
+            loop = c.get("ddp_loop", "native")
+            if loop == "peer":
+                # extension: the two ranks' update as one fused launch split across them; only for
+                # what ddrl_peer_attach supports, otherwise the all-reduce learner
+                why = [w for w, bad in (("a GraphNet model", self.cfg.model_kind != N.MODEL_FFN),
+                                        (f"{self.world} ranks (peer mode pairs exactly two)", self.world != 2),
+                                        (f"sgd_minibatch_size {self.cfg.sgd_minibatch_size} (not 128)",
+                                         self.cfg.sgd_minibatch_size != 128),
+                                        ("DDRL_UPDATE_SPLIT=1 (peer mode needs the row split)",
+                                         os.environ.get("DDRL_UPDATE_SPLIT") == "1")) if bad]
+                if why:
+                    import warnings
+                    warnings.warn(f"ddp_loop 'peer' does not support {', '.join(why)}: using the all-reduce "
+                                  "data-parallel learner")
+                    loop = "native" if rccl else "python"
+            if loop == "peer":
                 self.learner = PeerLearner(self.ctx, self.comm, 0, self.cfg.sgd_minibatch_size)
-            elif rccl and c.get("ddp_loop", "native") == "native":
+            elif rccl and loop == "native":
                 native_comm_init(self.ctx, self.comm)
                 self.learner = NativeDataParallelLearner(self.ctx, self.comm, 0, self.cfg.sgd_minibatch_size,
                                                          c.get("ddp_mode", "split"))
@@ -227,19 +241,9 @@ class PPOTrainer:
 
     def _gather_records(self):
         """All-gather every rank's records (rank-major) into the learner context's union batch."""
-        torch = self.torch
+        from .ddp import gather_records
         for p in range(self.cfg.n_policies):
-            src = self.rctx.records_tensor(p)
-            dst = self.ctx.records_tensor(p)
-            if self.world == 1:
-                dst.copy_(src)
-                continue
-            if self.comm.device == "cpu":   # gloo
-                parts = [torch.empty_like(src, device="cpu") for _ in range(self.world)]
-                self.comm.dist.all_gather(parts, src.cpu(), group=self.comm.group)
-                dst.copy_(torch.cat(parts).to(dst.device))
-            else:                           # RCCL: straight into the learner's record buffer
-                self.comm.dist.all_gather_into_tensor(dst, src, group=self.comm.group)
+            gather_records(self.comm, self.rctx.records_tensor(p), self.ctx.records_tensor(p))
 
     def _learn(self):
         if self.parallel == "ddp":

@@ -282,13 +282,22 @@ int ddrl_ppo_update_ddp(ddrl_ctx* ctx, int pid, const int32_t* shuffle_dev, cons
  *   ddrl_ppo_update_peer: shuffle_dev = this rank's nb * 64 row indices (minibatch slot b owns
  *     entries [64 b, 64 b + 64)), perm_dev[n_epochs][nb] = the slots, the same on both ranks.
  *     Both ranks must issue the same sequence of peer updates, and each launch needs its peer's
- *     launch to run concurrently (a wait abandoned after 3 s raises, with the snapshot restored). */
+ *     launch to run concurrently (a wait abandoned after 3 s raises, with the snapshot restored).
+ *     A failed peer update detaches the context: the next ddrl_ppo_update_peer is refused ("no
+ *     peer") until both ranks have called ddrl_peer_attach again, which clears the outboxes. */
 #define DDRL_PEER_HANDLE_BYTES 64
 int ddrl_peer_alloc(ddrl_ctx* ctx, void** gx_out, void* ipc_handle_out);
 int ddrl_peer_open(ddrl_ctx* ctx, const void* ipc_handle, void** gx_out);
 int ddrl_peer_attach(ddrl_ctx* ctx, void* gx, int rank, int nranks);
 int ddrl_ppo_update_peer(ddrl_ctx* ctx, int pid, const int32_t* shuffle_dev, const int32_t* perm_dev,
                          int n_epochs, int nb, float kl_coeff, int max_steps);
+
+/* The GraphNet context's minibatch step as it runs now: *on = 1 for the one-launch step (the
+ * gradient launch reduces over its tiles and runs clip + Adam in its tail), 0 for the three-launch
+ * step (k_gnn + k_gnn_reduce + k_gnn_adam) -- DDRL_GNN_TAIL=0, an occupancy or owner-list refusal,
+ * or a fallback after a failed one-launch step -- or before the first 128-row step has built
+ * the owner lists; 0 for an fcnet context. */
+int ddrl_gnn_one_launch(ddrl_ctx* ctx, int* on);
 
 /* Model forward (ModelV2.forward + value_function) on arbitrary rows:
  * obs_dev[n][d] (ffn; + node_dev[n] = leg index with leg_coupling) or X_dev[n][4][23] +

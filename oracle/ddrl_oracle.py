@@ -581,10 +581,15 @@ def standardize(x):
 # --------------------------------------------------------------------------------------
 def ppo_loss_rows(logits, value, actions, old_logits, old_logp, vf_preds, adv, vt,
                   kl_coeff, clip_param=0.2, vf_clip_param=10.0, vf_loss_coeff=0.5,
-                  entropy_coeff=0.0, vf_clip_mode="ray10"):
+                  entropy_coeff=0.0, vf_clip_mode="ray10", force=None):
     """Per-row loss terms and analytic dL/dlogits, dL/dvalue for L = mean over rows.
     The tie rules follow TF's gradient kernels: tf.minimum routes to x where x <= y,
-    tf.maximum to x where x >= y, clip_by_value passes for lo <= t <= hi."""
+    tf.maximum to x where x >= y, clip_by_value passes for lo <= t <= hi.
+
+    `force` (test infrastructure, the tie-following trajectory of DESIGN.md section 4): an
+    optional dict {"pol": {row: bool}, "vf": {row: bool}} that overrides whether a row's
+    surrogate / value term passes gradient -- the two clip decisions, whose outcome at a
+    near-tie (margin below fp32 resolution) depends on the implementation's rounding."""
     f = F32
     logits = np.asarray(logits, f)
     n, A2 = logits.shape
@@ -600,6 +605,9 @@ def ppo_loss_rows(logits, value, actions, old_logits, old_logp, vf_preds, adv, v
     s1, s2 = adv * ratio, adv * cr
     surr = np.minimum(s1, s2)
     d_ratio = np.where(s1 <= s2, adv, adv * ((ratio >= lo) & (ratio <= hi)))  # d surr
+    if force and force.get("pol"):
+        for i, on in force["pol"].items():
+            d_ratio[i] = adv[i] if on else 0.0
     var1 = np.square(np.exp(os_))
     kl = np.sum(log_std - os_ + (var1 + np.square(om - mean)) / (2 * std * std) - 0.5, 1)
     ent = np.sum(log_std + f(0.5 * np.log(2 * np.pi * np.e)), 1)
@@ -611,6 +619,9 @@ def ppo_loss_rows(logits, value, actions, old_logits, old_logp, vf_preds, adv, v
         vf = np.maximum(vf1, vf2)
         d_vf = np.where(vf1 >= vf2, 2 * (value - vt),
                         2 * (vclip - vt) * ((dv >= -vf_clip_param) & (dv <= vf_clip_param)))
+        if force and force.get("vf"):
+            for i, on in force["vf"].items():
+                d_vf[i] = (2 * (value[i] - vt[i]) if vf1[i] >= vf2[i] else 2 * (vclip[i] - vt[i])) if on else 0.0
     else:  # later RLlib: clip((V - VT)^2, 0, vf_clip)
         sq = np.square(value - vt)
         vf = np.clip(sq, 0, vf_clip_param)
@@ -628,6 +639,33 @@ def ppo_loss_rows(logits, value, actions, old_logits, old_logp, vf_preds, adv, v
                  kl=np.mean(kl), entropy=np.mean(ent),
                  vf_explained_var=explained_variance(vt, value))
     return dlogits.astype(f), dvalue.astype(f), stats
+
+
+def ppo_branches(logits, value, actions, old_logp, vf_preds, adv, vt, clip_param=0.2, vf_clip_param=10.0):
+    """Test infrastructure: each row's two clip decisions of ppo_loss_rows (ray10 value clip)
+    and their relative margins.  pol_on: the surrogate passes gradient (adv > 0: ratio <= 1 +
+    clip; adv < 0: ratio >= 1 - clip); vf_on: the value term passes gradient (vf1 >= vf2 or
+    |V - vf_old| <= vf_clip).  A margin is the signed relative distance of the deciding quantity
+    from its threshold; a decision is ambiguous in fp32 when its margin is within rounding."""
+    logits = np.asarray(logits, np.float64)
+    A = logits.shape[1] // 2
+    mean, log_std = logits[:, :A], logits[:, A:]
+    z = (np.asarray(actions, np.float64) - mean) / np.exp(log_std)
+    logp = -0.5 * np.sum(z * z, 1) - 0.5 * LOG2PI * A - np.sum(log_std, 1)
+    ratio = np.exp(logp - np.asarray(old_logp, np.float64))
+    adv = np.asarray(adv, np.float64)
+    lo, hi = 1.0 - clip_param, 1.0 + clip_param
+    pol_on = np.where(adv > 0, ratio <= hi, np.where(adv < 0, ratio >= lo, True))
+    pol_m = np.where(adv > 0, (hi - ratio) / hi, np.where(adv < 0, (ratio - lo) / lo, np.inf))
+    value = np.asarray(value, np.float64)
+    vf_preds, vt = np.asarray(vf_preds, np.float64), np.asarray(vt, np.float64)
+    dv = value - vf_preds
+    vcl = vf_preds + np.clip(dv, -vf_clip_param, vf_clip_param)
+    vf1, vf2 = (value - vt) ** 2, (vcl - vt) ** 2
+    m_sq = (vf1 - vf2) / np.maximum(np.maximum(vf1, vf2), 1e-30)     # > 0: vf1 wins
+    m_in = (vf_clip_param - np.abs(dv)) / vf_clip_param                # > 0: inside the clip
+    vf_on = (vf1 >= vf2) | (np.abs(dv) <= vf_clip_param)
+    return pol_on, pol_m, vf_on, m_sq, m_in
 
 
 def explained_variance(y, pred):

@@ -391,3 +391,90 @@ def strict_params_check(got, model, params, shapes, batch, sh, pe, kl, steps, cf
     if n_over:
         assert dev_hip.max() <= 2 * lr * steps + 1e-5, (msg, dev_hip.max())
     return n_over, n_ex, n
+
+
+def tie_following_trajectory(ctx, pid, params, shapes, batch, sh, pe, kl, steps, horizons, tol=2e-5,
+                             max_combo=6, log=None):
+    """The fp64 trajectory of the fcnet minibatch loop that takes the HIP kernel's outcome at every
+    clip decision whose fp64 margin is within `tol` ("Near-ties").
+
+    PPO's loss has two clip decisions per row, each a discontinuity of the gradient: the
+    surrogate passes gradient or not (ratio against 1 +- clip) and the value term passes gradient
+    or not (|V - vf_old| against vf_clip, and (V - vt)^2 against the clipped square).  When a
+    decision's deciding quantity lies within fp32 resolution of its threshold, its outcome is set
+    by the implementation's rounding -- TF's, numpy's, the HIP kernel's alike -- and a flip changes
+    that step's gradient by a finite amount; the trajectories bifurcate there.  This loop runs
+    the fp64 algorithm and, at every step with an ambiguous decision (relative margin < tol,
+    oracle.ppo_branches), asks the HIP kernel which way it went: the context is reset to the
+    starting state, a fused launch runs the first k steps (the HIP trajectory's state), and
+    ddrl_ppo_grad returns the HIP gradient of step k's minibatch; the fp64 gradient is formed for
+    every combination of the ambiguous decisions and the closest one is taken.  Everything else
+    is fp64 arithmetic of the unmodified algorithm.
+
+    Returns (snapshots {H: fp64 theta}, per-step fp64 stats, ties), ties = one record per
+    ambiguous decision: (step, kind, row, margin, fp64 outcome, HIP outcome, best / runner-up
+    gradient error).  The context's state is left arbitrary (callers reset it)."""
+    import torch
+    O64 = O.with_dtype(np.float64)
+    n = sum(int(np.prod(s)) for _, s in shapes)
+    theta0 = O.pack(params, shapes)
+    theta = theta0.astype(np.float64)
+    adam = O64.Adam(n)
+    epochs, nb = pe.shape
+    dsh = torch.from_numpy(np.ascontiguousarray(sh)).cuda()
+    dpe = torch.from_numpy(np.ascontiguousarray(pe)).cuda()
+    gbuf = torch.zeros(n, device="cuda")
+    snaps, stats, ties = {}, [], []
+    hset = set(horizons)
+    cols = ("actions", "logits", "logp", "vf_preds", "adv", "vt")
+    for k in range(steps):
+        rows = O.minibatch_rows(sh, pe, k // nb, k % nb)
+        p = O64.unpack(theta, shapes)
+        logits, value, cache = O64.ffn_forward(p, batch["obs"][rows])
+        args = [batch[c][rows] for c in cols]
+        pol_on, pol_m, vf_on, m_sq, m_in = O.ppo_branches(logits, value, args[0], args[2], args[3], args[4],
+                                                          args[5])
+        amb = [("pol", int(i), float(pol_m[i]), bool(pol_on[i])) for i in np.flatnonzero(np.abs(pol_m) < tol)]
+        vamb = ((np.abs(m_sq) < tol) & ~(m_in > tol)) | ((np.abs(m_in) < tol) & ~(m_sq > tol))
+        amb += [("vf", int(i), float(m_sq[i] if abs(m_sq[i]) < abs(m_in[i]) else m_in[i]), bool(vf_on[i]))
+                for i in np.flatnonzero(vamb)]
+        force = None
+        if amb:
+            assert len(amb) <= max_combo, ("too many ambiguous decisions in one step", k, amb)
+            ctx.params_set(pid, theta0)
+            ctx.adam_set(pid, np.zeros(n, np.float32), np.zeros(n, np.float32), 0.9, 0.999)
+            if k > 0:
+                P = ctx.cfg.n_policies
+                ctx.ppo_update(1 << pid, [dsh if q == pid else None for q in range(P)],
+                               [dpe if q == pid else None for q in range(P)], [kl] * P, max_steps=k)
+            r = torch.from_numpy(np.ascontiguousarray(rows)).cuda()
+            ctx.ppo_grad(pid, r, rows.size, kl, gbuf)
+            ctx.synchronize()
+            gh = gbuf.cpu().numpy().astype(np.float64)
+            errs = []
+            for combo in range(1 << len(amb)):
+                f = {"pol": {}, "vf": {}}
+                for j, (kind, i, _, nat) in enumerate(amb):
+                    f[kind][i] = nat if not (combo >> j) & 1 else not nat
+                dl, dv, _ = O64.ppo_loss_rows(logits, value, *args, np.float64(kl), force=f)
+                g = O64.ffn_backward(p, cache, dl, dv)
+                gf = np.concatenate([g[nm].reshape(-1) for nm, _ in shapes])
+                errs.append((float(np.abs(gf - gh).max()), combo, f))
+            errs.sort(key=lambda e: e[0])
+            best, combo, force = errs[0]
+            second = errs[1][0]
+            for j, (kind, i, m, nat) in enumerate(amb):
+                hip = nat if not (combo >> j) & 1 else not nat
+                ties.append((k, kind, i, m, nat, hip, best, second))
+                if log:
+                    log(f"step {k}: {kind} tie, row {i}, margin {m:.3g}, fp64 {'on' if nat else 'off'}, "
+                        f"HIP {'on' if hip else 'off'} (gradient error {best:.3g}, other outcome {second:.3g})")
+        dl, dv, st = O64.ppo_loss_rows(logits, value, *args, np.float64(kl), force=force)
+        g = O64.ffn_backward(p, cache, dl, dv)
+        clipped, gn = O64.clip_by_global_norm([g[nm] for nm, _ in shapes])
+        theta = adam.apply(theta, np.concatenate([c.reshape(-1) for c in clipped]))
+        st["grad_gnorm"] = float(gn)
+        stats.append(st)
+        if k + 1 in hset:
+            snaps[k + 1] = theta.copy()
+    return snaps, stats, ties

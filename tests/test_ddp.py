@@ -1,4 +1,4 @@
-"""Data-parallel learner (ddrl_amd.ddp) on CPU: world_size-2 gloo process groups.
+"""Data-parallel learner (ddrl_amd.ddp) on CPU: world_size-2 and -4 gloo process groups.
 
 The learner is driven with an oracle backend (gradients / clip + Adam from the numpy
 oracle, scaled to 1 / sgd_minibatch_size like ddrl_ppo_grad), so these tests check the
@@ -103,17 +103,17 @@ def _worker(rank, world, port, out_dir, mode, rows_local, epochs):
     dist.destroy_process_group()
 
 
-def _run(mode, rows_local, epochs):
+def _run(mode, rows_local, epochs, world=2):
     import torch.multiprocessing as mp
     out = tempfile.mkdtemp()
-    mp.spawn(_worker, args=(2, _free_port(), out, mode, rows_local, epochs), nprocs=2, join=True)
-    return [dict(np.load(os.path.join(out, f"r{r}.npz"))) for r in range(2)]
+    mp.spawn(_worker, args=(world, _free_port(), out, mode, rows_local, epochs), nprocs=world, join=True)
+    return [dict(np.load(os.path.join(out, f"r{r}.npz"))) for r in range(world)]
 
 
 def _reference(res, mode, rows_local, epochs):
-    """Single process: the union of both ranks' rows per step, one 128-row (split) or
-    256-row (local) minibatch gradient, clip + Adam."""
-    world = 2
+    """Single process: the union of every rank's rows per step, one 128-row (split) or
+    128 G-row (local) minibatch gradient, clip + Adam."""
+    world = len(res)
     m = MB // world if mode == "split" else MB
     batches = [_rank_batch(r, rows_local) for r in range(world)]
     full = {k: np.concatenate([b[k] for b in batches]) for k in batches[0]}
@@ -147,35 +147,82 @@ def _params_close(got, ref, steps):
     assert diff.max() <= 2 * 3e-4 * steps + 1e-5
 
 
-@pytest.mark.parametrize("mode", ["split", "local"])
-def test_ddp_learner_world2(mode):
+@pytest.mark.parametrize("world,mode", [(2, "split"), (2, "local"), (4, "split"), (4, "local")])
+def test_ddp_learner(world, mode):
+    """World 2 and world 4 (the ranks beyond two of the driver's 8-GPU run)."""
     rows_local, epochs = 512, 2
-    res = _run(mode, rows_local, epochs)
-    # identical parameters on both ranks (same all-reduced gradient, same Adam)
-    np.testing.assert_array_equal(res[0]["theta"], res[1]["theta"])
+    res = _run(mode, rows_local, epochs, world)
+    # identical parameters on every rank (same all-reduced gradient, same Adam)
+    for r in range(1, world):
+        np.testing.assert_array_equal(res[0]["theta"], res[r]["theta"])
+        assert res[0]["kl"] == res[r]["kl"]
     ref, kl_ref = _reference(res, mode, rows_local, epochs)
     steps = res[0]["perms"].size
     _params_close(res[0]["theta"], ref, steps)
     np.testing.assert_allclose(res[0]["kl"], kl_ref, rtol=1e-5)
-    assert res[0]["kl"] == res[1]["kl"]
     if mode == "split":
-        # filter sync == one RunningStat over base + rank 0 + rank 1 pushes
+        # filter sync == one RunningStat over base + every rank's pushes, in rank order
         rs = O.RunningStat((43,))
         for x in np.random.default_rng(0).normal(size=(50, 43)):
             rs.push(x)
-        for r in range(2):
+        for r in range(world):
             for x in np.random.default_rng(100 + r).normal(size=(30 + 7 * r, 43)) * 2 + r:
                 rs.push(x)
-        for r in range(2):
+        for r in range(world):
             assert res[r]["n"] == rs.n
             np.testing.assert_allclose(res[r]["M"], rs.M, rtol=1e-12, atol=1e-12)
             np.testing.assert_allclose(res[r]["S"], rs.S, rtol=1e-11)
         adv = np.concatenate([np.random.default_rng(200 + r).normal(size=500 + 100 * r).astype(np.float32) * 3 + 1
-                              for r in range(2)])
+                              for r in range(world)])
         _, mean, std = O.standardize(adv)
-        assert res[0]["mean"] == res[1]["mean"] and res[0]["den"] == res[1]["den"]
+        for r in range(1, world):
+            assert res[0]["mean"] == res[r]["mean"] and res[0]["den"] == res[r]["den"]
         np.testing.assert_allclose(res[0]["mean"], mean, rtol=1e-6)
         np.testing.assert_allclose(res[0]["den"], max(np.float32(1e-4), std), rtol=1e-6)
+
+
+def _gather_worker(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+    from ddrl_amd.ddp import Comm, gather_records, sync_standardize
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = Comm("cpu")
+    rows, stride = 200 * 12, 32
+    src = torch.from_numpy(np.random.default_rng(50 + rank).normal(size=(rows, stride)).astype(np.float32))
+    dst = torch.full((rows * world, stride), np.nan)
+    gather_records(comm, src, dst)
+    adv = src[:, 27].double()
+    mean, den = sync_standardize(comm, [adv.sum().item(), (adv * adv).sum().item(), adv.numel()])
+    bad = None
+    try:
+        gather_records(comm, src, torch.empty((rows * world + 1, stride)))
+    except ValueError as e:
+        bad = str(e)
+    np.savez(os.path.join(out_dir, f"g{rank}.npz"), dst=dst.numpy(), mean=mean, den=den, bad=bad or "")
+    dist.destroy_process_group()
+
+
+def test_gather_records_world4():
+    """Gather mode's record exchange at world 4 (gloo): every rank ends with the same union batch,
+    rank-major, and the same StandardizeFields constants as one process over the union; a
+    mis-sized union buffer is refused before any collective."""
+    import torch.multiprocessing as mp
+    from ddrl_amd.ddp import standardize_constants
+    world = 4
+    out = tempfile.mkdtemp()
+    mp.spawn(_gather_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    res = [dict(np.load(os.path.join(out, f"g{r}.npz"))) for r in range(world)]
+    union = np.concatenate([np.random.default_rng(50 + r).normal(size=(2400, 32)).astype(np.float32)
+                            for r in range(world)])
+    a = union[:, 27].astype(np.float64)
+    mean, den = standardize_constants([a.sum(), (a * a).sum(), a.size])
+    for r in range(world):
+        np.testing.assert_array_equal(res[r]["dst"], union)
+        assert res[r]["mean"] == res[0]["mean"] and res[r]["den"] == res[0]["den"]
+        np.testing.assert_allclose([res[r]["mean"], res[r]["den"]], [mean, den], rtol=1e-6)
+        assert "union buffer" in str(res[r]["bad"])
 
 
 def test_merge_running_stats_order_and_identity():
@@ -372,10 +419,16 @@ class _FakePeerCtx:
 
     def synchronize(self):
         from ddrl_amd.native import DdrlError
-        raise DdrlError("update kernel: an exchange ... was abandoned (simulated)")
+        if self.fail_rank >= 0:
+            raise DdrlError("update kernel: an exchange ... was abandoned (simulated)")
+
+    def params_get(self, pid):
+        # fail_rank < 0: both launches "complete" but the ranks' weights differ (a partial the
+        # peer never saw), which the learner's digest exchange must catch
+        return np.full(self.n_params[0], 1.0 + self.rank, np.float32)
 
 
-def _peer_fallback_worker(rank, world, port, out_dir, rows_local, epochs):
+def _peer_fallback_worker(rank, world, port, out_dir, rows_local, epochs, fail_rank=1):
     import torch
     import torch.distributed as dist
     from ddrl_amd.ddp import Comm, PeerLearner
@@ -385,7 +438,7 @@ def _peer_fallback_worker(rank, world, port, out_dir, rows_local, epochs):
     params = O.ffn_init(np.random.default_rng(7), D, 2 * A)
     shapes = O.ffn_param_shapes(D, 2 * A)
     be = OracleBackend(params, shapes, _rank_batch(rank, rows_local), cap=1024)
-    ctx = _FakePeerCtx(rank, 1, be.theta.size)
+    ctx = _FakePeerCtx(rank, fail_rank, be.theta.size)
     learner = PeerLearner(ctx, Comm("cpu"), 0, MB, backend=be)
     shuffle, perms = learner.schedule(np.random.default_rng(300 + rank), rows_local, epochs)
     with pytest.warns(UserWarning, match="per-step all-reduce"):
@@ -396,15 +449,19 @@ def _peer_fallback_worker(rank, world, port, out_dir, rows_local, epochs):
     dist.destroy_process_group()
 
 
-def test_peer_learner_falls_back_to_allreduce_loop_world2():
+@pytest.mark.parametrize("fail_rank", [1, -1])
+def test_peer_learner_falls_back_to_allreduce_loop_world2(fail_rank):
     """PeerLearner over gloo with a stand-in context: rank 0 allocates and attaches before rank 1
-    opens the handle and attaches; a refused peer launch on rank 1 (rank 0's waits abandoned)
-    makes BOTH ranks fall back to the per-step all-reduce learner for the same update, which
-    then matches the single-process union reference like test_ddp_learner_world2[split]."""
+    opens the handle and attaches; a refused peer launch on rank 1 (rank 0's waits abandoned) --
+    or (fail_rank -1) two launches that complete with different weights on the two ranks, caught
+    by the learner's weight-digest exchange -- makes BOTH ranks fall back to the
+    per-step all-reduce learner for the same update, which then matches the single-process union
+    reference like test_ddp_learner[2-split]."""
     import torch.multiprocessing as mp
     rows_local, epochs = 512, 2
     out = tempfile.mkdtemp()
-    mp.spawn(_peer_fallback_worker, args=(2, _free_port(), out, rows_local, epochs), nprocs=2, join=True)
+    mp.spawn(_peer_fallback_worker, args=(2, _free_port(), out, rows_local, epochs, fail_rank), nprocs=2,
+             join=True)
     res = [dict(np.load(os.path.join(out, f"r{r}.npz"))) for r in range(2)]
     assert list(res[0]["calls"][:2]) == ["alloc", "('attach', 4096, 0)"]
     assert list(res[1]["calls"][:2]) == ["open", "('attach', 8192, 1)"]
