@@ -81,6 +81,16 @@ def pmc_traffic(key, policy_steps):
     return w["hbm_bytes_per_step"] * policy_steps if w else None
 
 
+def pmc_ns_per_step(key, P):
+    """Duration per sequential minibatch step of the dominant kernel in the committed PMC pass
+    (its --kernel-trace duration over the pass's steps; P policies run side by side), or None."""
+    w, _ = pmc_workload(key)
+    m = (w or {}).get("mfma") or {}
+    if not m.get("duration_ns") or not w.get("steps"):
+        return None
+    return m["duration_ns"] / (w["steps"] / P)
+
+
 def pmc_mfma(key):
     """MFMA-busy and effective clock of the workload's dominant update kernel from the committed
     counter pass (SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE with --kernel-trace; see
@@ -581,6 +591,12 @@ def main():
                     f"of the records per iteration, the same fused update over the union batch of "
                     f"{n_local * world} envs on every rank (no per-step collective)" if gather else
                     "replicas (no collective)"))
+    # provenance of the committed counter pass: its kernel's duration per
+    # sequential step beside this run's; > 3 % apart marks `traffic` (and the MFMA-busy figures)
+    # as from another build or box
+    pmc_ns = None if ddp else pmc_ns_per_step(pkey, P)
+    meas_ns = mb_latency_ms * 1e6
+    stale = None if pmc_ns is None else abs(pmc_ns / meas_ns - 1.0) > 0.03
     result = {
         "metric": metric_name(args.envs),
         "value": env_steps / t_max,
@@ -609,6 +625,7 @@ def main():
             "frac": achieved_tf / PEAK_FP32_TFLOPS,
             "traffic": None if ddp else pmc_traffic(pkey, steps_per_policy * P),
             "traffic_source": None if ddp else f"{pmc_summary(pkey)[1]} [{pkey}] (bytes per step x steps of this update)",
+            "pmc_kernel_ns_per_step": pmc_ns, "measured_ns_per_step": meas_ns, "traffic_stale": stale,
             "algorithmic_flops_per_launch": flops_launch,
             "algorithmic_bytes_per_launch": rec_bytes_launch,
             "active_cus": active_cus,

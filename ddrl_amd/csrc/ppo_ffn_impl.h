@@ -719,6 +719,11 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
   constexpr int ROWS = DDRL_MB / KSP;
   constexpr int NT = Geo<NW, ROWS>::NT, RT = Geo<NW, ROWS>::RT, NS1 = Geo<NW, ROWS>::NS1, NS2 = Geo<NW, ROWS>::NS2;
   constexpr bool PAD = update_pad(A, KSP);   // layout of the weight images (common.h)
+#ifdef DDRL_ABL_NO_MOMENTS
+  constexpr bool NOMOM = KSP == 2;
+#else
+  constexpr bool NOMOM = false;
+#endif
   const int wkq = ub.own_kq < 0 ? 0 : ub.own_kq;   // the half that writes back and writes the statistics
   const UpdateHyper& H = ub.h;
   const int d = U.d;
@@ -1341,7 +1346,10 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const float2v gr = {gt[i][2 * h], gt[i][2 * h + 1]};
-          float2v m2 = {mt[i][2 * h], mt[i][2 * h + 1]}, v2 = {vt4[i][2 * h], vt4[i][2 * h + 1]};
+          // NOMOM: the timing-only cost model of VERDICT r05 item 3 -- the weight tiles' moments
+          // not carried across steps, i.e. their 2 x 4 x NTS VGPRs out of the step loop (wrong results)
+          float2v m2 = {NOMOM ? 0.f : mt[i][2 * h], NOMOM ? 0.f : mt[i][2 * h + 1]},
+                  v2 = {NOMOM ? 0.f : vt4[i][2 * h], NOMOM ? 0.f : vt4[i][2 * h + 1]};
           const float2v sc = {scale, scale}, k1 = {c1, c1}, k2 = {c2, c2}, al = {alpha, alpha};
           const float2v g = gr * sc;
           m2 = __builtin_elementwise_fma(__builtin_elementwise_fma(gr, sc, -m2), k1, m2);
@@ -1350,8 +1358,10 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
           den = den + (float2v){H.eps, H.eps};
           const float2v rc = {__builtin_amdgcn_rcpf(den[0]), __builtin_amdgcn_rcpf(den[1])};
           const float2v t2 = __builtin_elementwise_fma(-(m2 * al), rc, (float2v){th[i][2 * h], th[i][2 * h + 1]});
-          mt[i][2 * h] = m2[0]; mt[i][2 * h + 1] = m2[1];
-          vt4[i][2 * h] = v2[0]; vt4[i][2 * h + 1] = v2[1];
+          if constexpr (!NOMOM) {
+            mt[i][2 * h] = m2[0]; mt[i][2 * h + 1] = m2[1];
+            vt4[i][2 * h] = v2[0]; vt4[i][2 * h + 1] = v2[1];
+          }
           th[i][2 * h] = t2[0]; th[i][2 * h + 1] = t2[1];
         }
 
@@ -1404,8 +1414,10 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       const int f = 16 * tfa[i] + 4 * q + r, o = 16 * tfo[i] + c;
       if (!(tv[i] && (i < NS1 || f < d))) continue;
       const int pidx = (i < NS1 ? bo.w2 : bo.w1) + f * 64 + o;
-      U.m[pidx] = mt[i][r];
-      U.v[pidx] = vt4[i][r];
+      if constexpr (!NOMOM) {
+        U.m[pidx] = mt[i][r];
+        U.v[pidx] = vt4[i][r];
+      }
     }
 #pragma unroll
   for (int k = 0; k < NSLOT; ++k) {

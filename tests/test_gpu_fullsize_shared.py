@@ -17,26 +17,9 @@ against fp64 statistics of all advantages, and the first three fused steps again
 trajectory (tests/gpu_harness.strict_params_check).
 
 C4, one quarter epoch (6,400 steps, the horizon tests/test_gpu_longhorizon.py runs for Local):
-the same two-regime bar as that test.  Up to C4_ABS_BAR_UNTIL = 400 steps: within 4 e32(H) +
-2e-7 of fp64, 1e-5 absolute, statistics within 1e-4 relative.  Between 400 and 3,200 steps the
-trajectories bifurcate (a ratio / value clip of a row switches branch in fp32 but not in fp64;
-measured r05: HIP had left fp64 by 4e-3 at 1,600 while the first numpy fp32 run was still at
-1e-6, and at 3,200 five of eight fp32 row-order variants had jumped by 9e-3, three had not),
-so from 3,200 on the bar is the spread of TWENTY fp32 runs: the numpy run, seven that sum each
-minibatch's rows in another fixed order, eight that start from the same weights moved by one
-ulp (a random sign per entry: the rounding of another fp32 initialization), and four whose tanh
-is the kernels' own fp32 formula, 1 - 2 / (2^(2 log2(e) |x|) + 1) with the sign restored (error
-~1.5e-7 where numpy's is correctly rounded; DESIGN.md section 3 "Transcendentals").  The
-rounding-only variants fall into two discrete outcome classes (measured r05: row-order and
-one-ulp runs alike bifurcate at the same steps, after 1,600), while an implementation whose
-transcendentals carry ~1e-7 of error -- HIP's -- can bifurcate earlier; the fast-tanh runs
-sample that (measured r05: none of the twenty had bifurcated at 1,600, the fast-tanh ones
-included, while HIP had; at 3,200 twelve of twenty had jumped by 9e-3 and HIP sat at 9.7e-3;
-HIP / spread ratios 0.06 - 1.95).  HIP must stay within 2x that spread for the
-parameters and for the mean learner statistics over the 6,400 steps, every HIP / spread ratio
-printed and held to its recorded value + RATIO_MARGIN (R05_RATIO_C4).  H = 1,600 is printed
-(with how many fp32 runs have bifurcated), not asserted: the ensemble is still mostly in the
-deterministic regime there, so its spread is not the bar of a bifurcated trajectory.
+the absolute bar at every horizon against the fp64 trajectory that follows the kernel at clip
+near-ties (test_c4_quarter_epoch_against_tie_following_fp64 says why: the r05 departure at
+H = 680 is one value-clip decision whose fp64 margin is 1.1e-7).
 
 C5: the numpy GraphNet costs ~20 ms per step, so a whole-epoch oracle trajectory is out of
 reach; instead (a) 100 steps against fp64 (tests/gpu_harness.drift_check: HIP <= 4 e32 + 2e-7,
@@ -59,16 +42,11 @@ T = 200
 C4_ENV, C4_N = "QuantrupedMultiEnv_SharedDecentral", 4096
 C5_N = 2048
 HORIZONS = [10, 100, 400, 1600, 3200, 6400]
-C4_ABS_BAR_UNTIL = 400
-C4_SPREAD_FROM = 3200
-N_ROW_ORDER_VARIANTS = 7
-N_ULP_VARIANTS = 8
-N_FAST_TANH_VARIANTS = 4
+# relative margin below which a clip decision counts as a near-tie whose outcome is read off the
+# HIP gradient (tests/gpu_harness.tie_following_trajectory); the ties HIP took the other way from
+# fp64 measured r06 sit at |margin| <= 1.9e-6
+TIE_TOL = 1e-5
 STAT_KEYS = [(1, "policy_loss"), (2, "vf_loss"), (3, "kl"), (4, "entropy"), (6, "grad_gnorm")]
-# HIP distance to fp64 / 20-run fp32 spread at C4 (measured r05, profiles/r05/c4_quarter_epoch.log)
-R05_RATIO_C4 = {"theta@3200": 1.043, "theta@6400": 0.706, "policy_loss": 0.980, "vf_loss": 0.060, "kl": 1.566,
-                "entropy": 1.945, "grad_gnorm": 0.532}
-RATIO_MARGIN = 0.25
 _C5_STATS100 = {}   # the learner statistics of test_c5_100_steps_against_fp64's launch
 
 
@@ -238,8 +216,32 @@ def _run(mod, params, shapes, batch, sh, pe, horizons):
     return {h: np.asarray(v, np.float64) for h, v in snaps.items()}, stats
 
 
-def test_c4_quarter_epoch_against_fp64_trajectory(c4):
+@pytest.mark.timeout(600)
+def test_c4_quarter_epoch_against_tie_following_fp64(c4):
+    """the C4 departure at H = 680 is a value-clip near-tie.
+
+    Diagnosed in round 6 (tools/r06_c4_diag*.py, profiles/r06/): the HIP trajectory left the
+    fp64 one at step 679 because of one row (row 101 of that minibatch) whose |V - vf_old| is
+    10 (1 + 1.1e-7) in fp64 -- 1.1e-6 beyond vf_clip, about one ulp of 10 -- so fp64 and numpy
+    clip it (no value gradient) and the kernel, whose dot-product order rounds V the other way,
+    does not.  Neither the LSB-tagged exchange (a DDRL_UPDATE_SPLIT=1 launch, which has none, and
+    the one-rank pair path, which adds untouched partials, both reproduce or avoid the departure
+    with the row split, not the tags) nor the hardware rcp / sqrt (the numpy ensemble with Adam's
+    and the clip scale's rounding perturbed does not depart) is involved.
+
+    So the bar is the fp64 trajectory that takes the kernel's outcome at every clip decision
+    whose fp64 margin is below TIE_TOL (tests/gpu_harness.tie_following_trajectory: the decision
+    is read from the HIP gradient of that step, from the HIP trajectory's own state).  Against it
+    the absolute bar holds at EVERY horizon through the quarter epoch (6,400 steps): within
+    4 e32(H) + 2e-7 and 1e-5 of it, where e32(H) = the numpy fp32 run's distance from the plain
+    fp64 trajectory, and every step's learner statistics within 1e-4 relative (+1e-6).  The ties
+    HIP took the other way from fp64 are printed with their margins (measured r06: 5 of 1,995
+    ambiguous decisions, |margin| <= 1.9e-6).  The plain-fp64 distances and a four-run fp32
+    ensemble are printed for context; the mean statistics' HIP / spread ratios use the
+    tie-following trajectory (HIP's distance from the fp64 path of its own tie decisions over the
+    ensemble's spread around plain fp64) and must stay below 1.5."""
     import torch
+    from tests.gpu_harness import tie_following_trajectory
     ctx, cfg, params, _, rec = c4
     d, A = cfg.obs_dim[0], cfg.act_dim
     shapes = O.ffn_param_shapes(d, 2 * A)
@@ -248,63 +250,60 @@ def test_c4_quarter_epoch_against_fp64_trajectory(c4):
     batch = _ffn_batch(rec, lay, d, A, ctx.adv_norm_get(0))
     R = rec.shape[0]
     sh, pe = O.sgd_schedule(np.random.default_rng(44), R, 128, 10)
+    H_MAX = max(HORIZONS)
     O64 = O.with_dtype(np.float64)
     th64, st64 = _run(O64, {k: v.astype(np.float64) for k, v in params.items()}, shapes, batch, sh, pe, HORIZONS)
-    late = [h for h in HORIZONS if h > C4_ABS_BAR_UNTIL]
-    runs32 = [_run(O, params, shapes, batch, sh, pe, HORIZONS)]
-    runs32 += [_run(O, params, shapes, batch, _row_order_variant(sh, 90 + k), pe, late)
-               for k in range(N_ROW_ORDER_VARIANTS)]
-    runs32 += [_run(O, _ulp_variant(params, 200 + k), shapes, batch, sh, pe, late) for k in range(N_ULP_VARIANTS)]
-    OF = _fast_tanh_oracle()
-    runs32 += [_run(OF, params, shapes, batch, sh if k == 0 else _row_order_variant(sh, 300 + k), pe, late)
-               for k in range(N_FAST_TANH_VARIANTS)]
+    runs32 = [_run(O, params, shapes, batch, sh, pe, HORIZONS),
+              _run(O, params, shapes, batch, _row_order_variant(sh, 90), pe, HORIZONS),
+              _run(O, _ulp_variant(params, 200), shapes, batch, sh, pe, HORIZONS),
+              _run(_fast_tanh_oracle(), params, shapes, batch, sh, pe, HORIZONS)]
+    tf, tst, ties = tie_following_trajectory(ctx, 0, params, shapes, batch, sh, pe, 0.2, H_MAX, HORIZONS,
+                                             tol=TIE_TOL)
+    flips = [t for t in ties if t[4] != t[5]]
+    print(f"\nC4 tie-following fp64 trajectory: {len(ties)} clip decisions within {TIE_TOL:g} of their threshold, "
+          f"{len(flips)} taken the other way by HIP:")
+    for k, kind, i, m, nat, hip, best, second in flips:
+        print(f"  step {k}: {'value' if kind == 'vf' else 'surrogate'} clip of minibatch row {i}, fp64 margin "
+              f"{m:.3g}, fp64 {'passes' if nat else 'clips'}, HIP {'passes' if hip else 'clips'} (HIP gradient vs "
+              f"fp64 with HIP's outcome {best:.3g}, with fp64's {second:.3g})")
+    fails = []
+    # every decision was read unambiguously off the HIP gradient
+    for t in ties:
+        if not t[6] <= 0.1 * t[7]:
+            fails.append(("undecided tie", t))
     dsh, dpe = torch.from_numpy(sh).cuda(), torch.from_numpy(pe).cuda()
-    ratios, fails = {}, []
-
-    def ratio(name, dist, spread):
-        r = dist / spread if spread > 0 else (0.0 if dist == 0 else np.inf)
-        ratios[name] = r
-        cap = min(2.0, R05_RATIO_C4.get(name, 2.0 - RATIO_MARGIN) + RATIO_MARGIN)
-        if not (r <= cap or dist <= 2e-7):
-            fails.append((name, r, cap))
-
     st = None
     for H in HORIZONS:
         _reset(ctx, theta0)
         ctx.ppo_update(1, [dsh], [dpe], [0.2], max_steps=H)
         ctx.synchronize()
         got = ctx.params_get(0).astype(np.float64)
-        egpu = np.abs(got - th64[H]).max()
-        e32s = [np.abs(r[0][H] - th64[H]).max() for r in runs32 if H in r[0]]
-        d32 = np.abs(got - runs32[0][0][H]).max()
-        print(f"\nC4 H={H}: max dev from fp64: numpy fp32 runs {[f'{e:.3g}' for e in e32s]}, HIP {egpu:.3g} "
-              f"({np.mean(np.abs(got - th64[H]) <= 1e-5):.4f} within 1e-5); max |HIP - numpy fp32| {d32:.3g}",
-              flush=True)
+        e32 = np.abs(runs32[0][0][H] - th64[H]).max()
+        etf = np.abs(got - tf[H]).max()
+        e64 = np.abs(got - th64[H]).max()
+        ens = [np.abs(r[0][H] - th64[H]).max() for r in runs32]
+        print(f"C4 H={H}: HIP - tie-following fp64 {etf:.3g} (bar {4 * e32 + 2e-7:.3g}); HIP - plain fp64 {e64:.3g}; "
+              f"fp32 runs - plain fp64 {[f'{e:.3g}' for e in ens]}", flush=True)
+        if not (etf <= 4 * e32 + 2e-7 and etf <= 1e-5):
+            fails.append((f"theta@{H}", etf, e32))
         st = ctx.ppo_stats(0, H).astype(np.float64)
-        if H <= C4_ABS_BAR_UNTIL:
-            if not (egpu <= 4 * e32s[0] + 2e-7 and egpu <= 1e-5 and d32 <= 1e-6):
-                fails.append((f"theta@{H}", egpu, e32s[0], d32))
-            for col, k in STAT_KEYS:
-                ref = np.array([s[k] for s in st64[:H]])
-                dev = np.abs(st[:, col] - ref)
-                if not np.all(dev <= 1e-4 * np.abs(ref) + 1e-6):
-                    fails.append((f"{k}@{H}", dev.max()))
-        elif H < C4_SPREAD_FROM:
-            print(f"C4 H={H}: {sum(e > 1e-4 for e in e32s)} of {len(e32s)} fp32 runs bifurcated (printed only)")
-        else:
-            if not egpu <= 2 * max(e32s) + 2e-7:
-                fails.append((f"theta@{H} 2x spread", egpu, max(e32s)))
-            ratio(f"theta@{H}", egpu, max(e32s))
+        for col, k in STAT_KEYS:
+            ref = np.array([s[k] for s in tst[:H]])
+            dev = np.abs(st[:, col] - ref)
+            if not np.all(dev <= 1e-4 * np.abs(ref) + 1e-6):
+                j = int(np.argmax(dev - 1e-4 * np.abs(ref)))
+                fails.append((f"{k}@{H}", j, st[j, col], ref[j]))
+    ratios = {}
     for col, k in STAT_KEYS:   # mean statistics over the 6,400 steps
-        ref = np.mean([s[k] for s in st64])
-        dg = abs(st[:, col].mean() - ref)
-        spread = max(abs(np.mean([s[k] for s in r[1]]) - ref) for r in runs32)
-        print(f"C4 mean {k} over 6400 steps: |HIP - fp64| {dg:.3g}, fp32 spread {spread:.3g} (ref {ref:.4g})")
-        if not dg <= 2 * spread + 2e-7 * abs(ref):
-            fails.append((f"mean {k} 2x spread", dg, spread))
-        ratio(k, dg, spread)
-    print("C4 HIP / fp32-spread ratios (recorded in parentheses): " +
-          ", ".join(f"{k} {v:.3f} ({R05_RATIO_C4.get(k, float('nan')):.2f})" for k, v in ratios.items()), flush=True)
+        ref64 = np.mean([s[k] for s in st64])
+        reftf = np.mean([s[k] for s in tst])
+        dg = abs(st[:, col].mean() - reftf)
+        spread = max(abs(np.mean([s[k] for s in r[1]]) - ref64) for r in runs32)
+        ratios[k] = dg / spread if spread > 0 else (0.0 if dg == 0 else np.inf)
+        print(f"C4 mean {k} over {H_MAX} steps: |HIP - tie-following fp64| {dg:.3g}, |HIP - plain fp64| "
+              f"{abs(st[:, col].mean() - ref64):.3g}, fp32 ensemble spread {spread:.3g} (ratio {ratios[k]:.3f})")
+        if not (ratios[k] < 1.5 or dg <= 2e-7 * abs(reftf)):
+            fails.append((f"mean {k} ratio", ratios[k]))
     assert not fails, fails
 
 

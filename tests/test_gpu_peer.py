@@ -143,10 +143,20 @@ def test_peer_update_without_its_peer_fails_and_restores(setup):
     gx, _ = ctx.peer_alloc()
     ctx.peer_attach(gx, 0, 2)
     ctx.ppo_update_peer(0, dev(S["sh"][0]), dev(S["pe"]), 0.2, max_steps=3)
-    with pytest.raises(DdrlError, match="as before the call"):
+    with pytest.raises(DdrlError, match="as before the call") as ei:
         ctx.synchronize()
+    assert "ddrl_peer_attach again" in str(ei.value)
     for x, y in zip(before, _state(ctx)):
         np.testing.assert_array_equal(np.asarray(x), np.asarray(y))
+    # the failed launch may have left partly written outboxes, so the context is
+    # detached -- a retry without re-attaching is refused before any launch, the state unchanged
+    with pytest.raises(DdrlError, match="no peer"):
+        ctx.ppo_update_peer(0, dev(S["sh"][0]), dev(S["pe"]), 0.2, max_steps=3)
+    for x, y in zip(before, _state(ctx)):
+        np.testing.assert_array_equal(np.asarray(x), np.asarray(y))
+    # re-attaching (rank 0 clears the outboxes) is accepted again
+    ctx.peer_attach(gx, 0, 2)
+    ctx.synchronize()
 
 
 def _peer_rank(rank, world, port, out_dir):

@@ -405,3 +405,40 @@ def test_oracle_reproduces_golden_vectors():
         close(new, z[pre + "new_params"])
         close(np.array([st["total_loss"], st["policy_loss"], st["vf_loss"], st["kl"], st["entropy"],
                         st["vf_explained_var"], gn], np.float32), z[pre + "stats"])
+
+
+def test_ppo_branches_and_forced_decisions():
+    """The tie-following trajectory's oracle hooks (tests/gpu_harness.tie_following_trajectory):
+    ppo_branches reports each row's two clip decisions consistently with ppo_loss_rows' gradient
+    (a row whose surrogate / value term is 'off' has zero d_ratio / d_vf), forcing every row to its
+    own decision changes nothing bit for bit, and flipping one row's decision changes only that
+    row's output gradient."""
+    rng = np.random.default_rng(3)
+    n, A = 64, 2
+    logits = np.concatenate([rng.normal(size=(n, A)) * 0.3, rng.normal(size=(n, A)) * 0.2 - 0.5], 1).astype(np.float32)
+    old = logits + rng.normal(size=logits.shape).astype(np.float32) * 0.3
+    act = rng.normal(size=(n, A)).astype(np.float32)
+    old_logp = O.dg_logp(old, act)
+    vf_old = rng.normal(size=n).astype(np.float32) * 5
+    value = (vf_old + rng.normal(size=n) * 12).astype(np.float32)
+    vt = (vf_old + rng.normal(size=n) * 8).astype(np.float32)
+    vt[::2] = value[::2] + rng.normal(size=n // 2).astype(np.float32)   # near V: clipped rows lose
+    adv = rng.normal(size=n).astype(np.float32)
+    args = (logits, value, act, old, old_logp, vf_old, adv, vt, np.float32(0.2))
+    dl, dv, _ = O.ppo_loss_rows(*args)
+    pol_on, pol_m, vf_on, m_sq, m_in = O.ppo_branches(logits, value, act, old_logp, vf_old, adv, vt)
+    assert 0 < pol_on.sum() < n and 0 < vf_on.sum() < n       # both kinds of decision occur
+    assert np.all(dv[~vf_on] == 0) and np.all(dv[vf_on] != 0)
+    # the policy term's share of dlogits vanishes exactly when the surrogate is clipped (beta-only rows)
+    dl_nokl, _, _ = O.ppo_loss_rows(*args[:-1], np.float32(0.0))
+    assert np.all(dl_nokl[~pol_on] == 0) and np.all(np.abs(dl_nokl[pol_on]).sum(1) > 0)
+    assert np.all((pol_m >= 0) == pol_on) and np.all(((m_sq >= 0) | (m_in >= 0)) == vf_on)
+    same = {"pol": {i: bool(pol_on[i]) for i in range(n)}, "vf": {i: bool(vf_on[i]) for i in range(n)}}
+    dl2, dv2, _ = O.ppo_loss_rows(*args, force=same)
+    np.testing.assert_array_equal(dl2, dl)
+    np.testing.assert_array_equal(dv2, dv)
+    i = int(np.flatnonzero(~vf_on)[0])
+    j = int(np.flatnonzero(pol_on)[0])
+    dl3, dv3, _ = O.ppo_loss_rows(*args, force={"vf": {i: True}, "pol": {j: False}})
+    assert dv3[i] != 0 and np.array_equal(np.delete(dv3, i), np.delete(dv, i))
+    assert not np.array_equal(dl3[j], dl[j]) and np.array_equal(np.delete(dl3, j, 0), np.delete(dl, j, 0))

@@ -1,8 +1,8 @@
 #!/bin/bash
-# r05 A/B timing: the default library against the in-tree variant builds named on the command line
+# r06 A/B timing: the default library against the in-tree variant builds named on the command line
 # (tools/ablate.py build), Local and C4 update us/step at 4096 envs, three alternating rounds; the
 # state digest shows bit-identity.
-O=gpurun_out/r05/ab
+O=gpurun_out/r06/ab
 mkdir -p $O
 for i in 1 2 3; do
   for v in default "$@"; do
