@@ -1012,6 +1012,24 @@ int ddrl_ppo_stats_range(ddrl_ctx* c, int pid, size_t first, size_t n_steps, flo
   return 0;
 }
 
+// Grow policy pid's learner-statistics buffer to at least `rows` rows, keeping its contents.  A
+// data-parallel loop in "split" mode runs 128 / (128 / G) = G times the fused schedule's
+// minibatches per epoch, which passes the buffer sized at create (num_sgd_iter x R / 128 rows)
+// when G > num_sgd_iter (found by the world-4 rehearsal with one epoch, round 6).  Growing waits
+// for the context's stream; it happens once per size.
+static int stats_reserve(ddrl_ctx* c, int pid, size_t rows) {
+  Policy& P = c->pol[pid];
+  if (rows <= P.stats_steps) return 0;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  float* nw = nullptr;
+  if (dalloc(c, &nw, rows * 8)) return -1;
+  if (P.stats_steps) HIPCHK(hipMemcpy(nw, P.stats, P.stats_steps * 8 * sizeof(float), hipMemcpyDeviceToDevice));
+  dfree(c, &P.stats);
+  P.stats = nw;
+  P.stats_steps = rows;
+  return 0;
+}
+
 // Workgroups per branch of a gradient-only update launch: the row split of the fused update
 // when the rows fill both halves (64 each), else one.  ddrl_ppo_grad and ddrl_ppo_update_ddp
 // share this rule, so the two data-parallel loops run the same kernels.
@@ -1023,7 +1041,9 @@ int ddrl_ppo_grad(ddrl_ctx* c, int pid, const int32_t* rows, int n_rows, float k
   if (pid < 0 || pid >= c->cfg.n_policies) return fail("bad policy id");
   if (n_rows < 1 || n_rows > 128) return fail("n_rows must be in [1, 128]");
   if (!rows || !grad) return fail("null rows/grad");
-  if (stats_step >= (int)c->pol[pid].stats_steps) return fail("stats_step beyond the stats buffer");
+  if (stats_step >= 0 && (size_t)stats_step >= c->pol[pid].stats_steps &&
+      stats_reserve(c, pid, std::max((size_t)stats_step + 1, 2 * c->pol[pid].stats_steps)))
+    return -1;
   UpdateArgs u = make_update(c, pid, rows, c->zero_perm, kl);
   u.nb = 1; u.n_epochs = 1; u.max_steps = 1; u.step0 = 0; u.grad_out = grad;
   c->snap_mask = 0;   // a gradient launch changes no state: the caller's loop keeps its own snapshot
@@ -1085,7 +1105,7 @@ int ddrl_ppo_update_ddp(ddrl_ctx* c, int pid, const int32_t* shuffle, const int3
   if (!c->comm) return fail("no communicator (ddrl_comm_init)");
   if (!shuffle || !perm || E < 1 || nb < 1) return fail("bad schedule");
   if (m < 1 || m > 128) return fail("rows_per_rank must be in [1, 128]");
-  if ((size_t)nb > c->pol[pid].stats_steps) return fail("more minibatches than the stats buffer holds");
+  if (stats_reserve(c, pid, (size_t)nb)) return -1;   // the last epoch's rows
   Policy& P = c->pol[pid];
   const int steps = E * nb;
   const UpdateHyper h = make_hyper(c, 1);

@@ -560,6 +560,42 @@ __device__ __forceinline__ void gnn_tile(const GnnArgs& ga, float* lds, const in
     ga.statp[(NET * (DDRL_MB / 4) + tile) * 8 + tid] = s;
   }
   float* P = ga.part + (size_t)tile * ga.part_stride;
+#ifdef DDRL_ABL_GNN_FWD_HANDOFF
+  // Timing-only cost model (results wrong): one forward per tile shared by
+  // its GNN_Z backward shares through the XCD's L2.  Share 0 publishes 16 KB (the size of a net's
+  // dz / h / du / dm images for a tile) and a tagged flag in the padding of its partial row; the
+  // other shares wait for the flag and read the 16 KB back.  Every share still runs its own
+  // forward above: the forward is on the step's critical path either way (the shares wait for
+  // share 0's), so this build adds exactly the hand-off.  The payload lands in partial slots that
+  // the real partial stores overwrite later.
+  if (ga.tail) {
+    unsigned* hf = reinterpret_cast<unsigned*>(P + ga.n_params + NET);
+    if (zs == 0) {
+      for (int i = tid; i < 4096; i += 256) P[i] = lds[i];
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(hf, ga.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (tid == 0) {
+        const unsigned long long h0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(hf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ga.tag) {
+          if (__builtin_amdgcn_s_memrealtime() - h0 > 300000000ull) {
+            __hip_atomic_store(ga.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __syncthreads();
+      float acc = 0.f;
+      for (int i = tid; i < 4096; i += 256)
+        acc += __uint_as_float(__hip_atomic_load(reinterpret_cast<const unsigned*>(P + i), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT));
+      if (acc == 1.2345e-30f) lds[L_ST + 40] = acc;   // keeps the loads
+      __syncthreads();
+    }
+  }
+#endif
   const bool is_sel = n == sel;
   float ds[O];
 #pragma unroll
@@ -1200,7 +1236,13 @@ __device__ __forceinline__ void gnn_tail(const GnnArgs& ga, float* lds, int tile
   // every reducer's norm^2 partial (one granule per thread), then the norm in a fixed order
   const int nr_all = ga.rbase[8];
   float gv = 0.f;
+#ifdef DDRL_ABL_GNN_LOCAL_NORM
+  // timing-only cost model (results wrong): the norm from this XCD's own
+  // reducers only -- no granule crosses an XCD
+  const bool ok2 = tid < ga.rbase[k] || tid >= ga.rbase[k + 1] || gnn_wait_gran(ga, ga.gran + tid, t0, gv);
+#else
   const bool ok2 = tid >= nr_all || gnn_wait_gran(ga, ga.gran + tid, t0, gv);
+#endif
   T[64 + tid] = gv;
   if (!__syncthreads_and(ok2)) return;
   RSTAMPB(gi, 2);
@@ -1295,6 +1337,11 @@ static GnnArgs grad_args(const UpdateArgs& u, const UpdateHyper& h, int step, in
                          const GnnScratch& sc, const float* stage, int layer) {
   GnnArgs ga{};
   ga.theta = u.theta; ga.u = u; ga.h = h; ga.step = step; ga.n_graphs = nrows; ga.inv_n = inv_n;
+#ifdef DDRL_ABL_GNN_THETA_RO
+  // timing-only cost model (results wrong): the tiles read their weights
+  // from a buffer no launch writes (the records), as if theta stayed in the reading XCD's L2
+  ga.theta = u.rec;
+#endif
   ga.part = sc.part; ga.part_stride = sc.part_stride; ga.statp = sc.statp; ga.normp = sc.normp;
   ga.bp_cur = sc.bp_cur; ga.grad = u.grad_out ? u.grad_out : sc.grad;
   ga.stage = stage;

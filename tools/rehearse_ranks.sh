@@ -22,7 +22,10 @@ for n in ${RANKS:-4 8}; do
   run "$n" "c4_gather_w$n.log" --env QuantrupedMultiEnv_SharedDecentral --envs 1024 --steps 1 --warmup 1
   run "$n" "c4_ddp_split_w$n.log" --env QuantrupedMultiEnv_SharedDecentral --envs 256 --steps 1 --warmup 1 \
     --shared-mode ddp --ddp-mode split --sgd-iter 1
-  run "$n" "c5_gather_w$n.log" --env QuantrupedMultiEnv_DecentralShared_Graph --envs 256 --steps 1 --warmup 1
+  # ranks sharing one GPU cannot all hold the one-launch GNN step's 256-block grid resident (its
+  # waits would end at their 3 s bound; the bench then reruns the update on three launches), so
+  # the shared-GPU rehearsal runs the three-launch step; on the 8-GPU node every rank has a GPU
+  DDRL_GNN_TAIL=0 run "$n" "c5_gather_w$n.log" --env QuantrupedMultiEnv_DecentralShared_Graph --envs 256 --steps 1 --warmup 1
 done
 unset DDRL_DIST_BACKEND
 run 1 n1_torchrun.log --steps 2 --warmup 1 --no-cpu-baseline
