@@ -54,6 +54,13 @@
 // the peer TU: atomic granules for the norm exchange and the gradient launches' pairs, quads at
 // system scope for the fused launches' partner exchange
 #define DDRL_XCHG_LXSYS (DDRL_FFN_AT == 2)
+// DDRL_ABL_PEER4: the timing-only cost model of a four-rank peer mode, in the
+// peer TU only: the weight-gradient K of a 32-row share and two more partners' quad reads at
+// system scope (the four-way split model of DESIGN.md section 6.2 on the peer protocol)
+#if defined(DDRL_ABL_PEER4) && DDRL_FFN_AT == 2
+#define DDRL_ABL_HALF_DW
+#define DDRL_ABL_XCHG3
+#endif
 #define DDRL_LX_ON (!DDRL_XCHG_IS_ATOMIC || DDRL_XCHG_LXSYS)
 
 namespace {
