@@ -41,7 +41,7 @@ def metric_name(envs):
     return f"env-steps/sec at {envs} envs × 4 leg agents; PPO update ms/minibatch"
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense FP32 (MFMA f32 = vector rate), MI355X_MICROARCH.md
 PEAK_HBM_GBS = 8000.0
-PMC_SUMMARIES = [os.path.join(ROOT, "profiles", r, "pmc_summary.json") for r in ("r05", "r04", "r03")]
+PMC_SUMMARIES = [os.path.join(ROOT, "profiles", r, "pmc_summary.json") for r in ("r06", "r05", "r04", "r03")]
 PMC_WORKLOAD = {"QuantrupedMultiEnv_Local": "local", "QuantrupedMultiEnv_SharedDecentral": "c4",
                 "QuantrupedMultiEnv_DecentralShared_Graph": "c5"}
 
@@ -73,7 +73,7 @@ def pmc_workload(key):
 
 def pmc_traffic(key, policy_steps):
     """HBM bytes of the update (all its launches) from the committed rocprofv3 PMC passes
-    (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE; tools/profile_r05.sh): the
+    (FETCH_SIZE x 2 per the gfx950 correction + WRITE_SIZE; tools/profile_r06.sh): the
     workload's bytes per (policy, minibatch) step times this update's steps -- the kernels'
     traffic is per step.  The counters cannot be read live from inside the timed run; None
     for a workload without a committed pass."""

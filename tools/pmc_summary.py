@@ -1,7 +1,7 @@
 """Per-step HBM traffic, matrix-core busy fraction and effective clock of the update kernels from
-the rocprofv3 PMC passes of tools/profile_r05.sh (earlier rounds: profile_r02.sh - r04.sh).
+the rocprofv3 PMC passes of tools/profile_r06.sh (earlier rounds: profile_r02.sh - r04.sh).
 
-    python tools/pmc_summary.py gpurun_out/prof5 > profiles/r05/pmc_summary.json
+    python tools/pmc_summary.py gpurun_out/prof6 > profiles/r06/pmc_summary.json
 
 Traffic: FETCH_SIZE and WRITE_SIZE come from separate passes (kB per dispatch); FETCH_SIZE is
 doubled per MI355X_MICROARCH.md (gfx950 tallies 128-B requests at 64 B).  Per workload the
@@ -60,7 +60,7 @@ WORKLOADS = {
                    "mfma": {"kernel": "void k_gnn<2, 2", "active_simds": 1024, "flop_per_step": 764800 * 128},
                    "also": ["k_gnn_reduce", "k_gnn_adam"]},
 }
-# LDS / issue counters (tools/profile_r05.sh "lds" passes), summed per kernel over its dispatches
+# LDS / issue counters (tools/profile_r06.sh "lds" passes), summed per kernel over its dispatches
 DETAIL = {"local": "void k_update_ffn<2, 9", "c5": "void k_gnn<2, 2"}
 DETAIL_COUNTERS = ["SQ_LDS_BANK_CONFLICT", "SQ_ACTIVE_INST_LDS", "SQ_INSTS_LDS", "SQ_LDS_ADDR_CONFLICT",
                    "SQ_INSTS_MFMA", "SQ_INSTS_VALU", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_ANY"]
@@ -161,7 +161,7 @@ def main(d):
         if st and st.get("clock_ghz"):
             LONG_CLOCK_GHZ = st["clock_ghz"]
             break
-    out = {"command": "tools/profile_r05.sh: rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | "
+    out = {"command": "tools/profile_r06.sh: rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | "
                       "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE (separate passes, "
                       "--kernel-trace) -- python3 bench.py --steps 1 --warmup 0 ...",
            "gfx950_fetch_correction": GFX950_FETCH_CORRECTION, "workloads": {}}

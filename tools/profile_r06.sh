@@ -1,17 +1,17 @@
 #!/bin/bash
-# Round-5 profile recipe (GPU box, repo root).  Kernel-trace stats of Local (C2/C3), C4 and C5
+# Round-6 profile recipe (the round-5 recipe on the round-6 build) (GPU box, repo root).  Kernel-trace stats of Local (C2/C3), C4 and C5
 # (2048 envs: one launch, and three launches with DDRL_GNN_TAIL=0); per workload one PMC pass per
 # TCC counter (FETCH_SIZE / WRITE_SIZE do not fit one pass) and one of the matrix-core / clock
 # counters, all with --kernel-trace; one pass of LDS / issue counters for the Local update and the
 # C5 gradient launch.  The C5 passes run the bench configuration (2048 envs, T = 200) for one
 # epoch (--sgd-iter 1: 12,800 steps).  Summary:
-#   gpurun_out/prof5/pmc_summary.json (tools/pmc_summary.py over the raw passes in /tmp/prof5)
+#   gpurun_out/prof6/pmc_summary.json (tools/pmc_summary.py over the raw passes in /tmp/prof6)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 # raw counter / trace CSVs stay in /tmp (hundreds of MB); the summary, the kernel stats and the
-# logs go to gpurun_out/prof5
-OUT=/tmp/prof5
-KEEP=$R/gpurun_out/prof5
+# logs go to gpurun_out/prof6
+OUT=/tmp/prof6
+KEEP=$R/gpurun_out/prof6
 mkdir -p $OUT $KEEP
 cd /tmp && export TMPDIR=/tmp
 LOCAL="--steps 1 --warmup 0 --no-cpu-baseline --no-pcie"
