@@ -43,6 +43,7 @@ pytestmark = pytest.mark.gpu
 N_ENVS, T = 4096, 200
 HORIZONS = [10, 100, 400, 1600, 3200, 6400]
 ABS_BAR_UNTIL = 1600
+TIE_TOL = 1e-5   # as tests/test_gpu_fullsize_shared.py
 STAT_KEYS = [(1, "policy_loss"), (2, "vf_loss"), (3, "kl"), (4, "entropy"), (6, "grad_gnorm")]
 # HIP distance to fp64 / fp32 spread, r03 kernel (profiles/r03/gpu_tests.log:118-127)
 R03_RATIO = {"theta@3200": 1.00, "theta@6400": 0.89, "logits": 0.93, "value": 1.10, "policy_loss": 0.33,
@@ -90,7 +91,8 @@ def _run(mod, params, shapes, batch, sh, pe, horizons):
     return {h: np.asarray(v, np.float64) for h, v in snaps.items()}, stats
 
 
-def test_one_epoch_local_fullsize_against_fp64_trajectory():
+@pytest.fixture(scope="module")
+def local():
     import torch
     from ddrl_amd.synthetic import SyntheticRollout
     ctx, cfg, inst = make_ctx("QuantrupedMultiEnv_Local", N_ENVS, T)
@@ -100,14 +102,23 @@ def test_one_epoch_local_fullsize_against_fp64_trajectory():
     ctx.rollout_fragment(syn.obs, syn.eps, syn.fw, syn.cfrc, syn.dones_for_fragment(), syn.actions)
     ctx.gae()
     ctx.synchronize()
+    del syn
     R = T * ctx.layout[0]["C"]
     assert R == 819200
     sched = [O.sgd_schedule(np.random.default_rng(40 + p), R, 128, 10) for p in range(4)]
+    p, d, A = 0, cfg.obs_dim[0], cfg.act_dim
+    batch = _batch(ctx.records_get(p), ctx.layout[p], d, A, ctx.adv_norm_get(p))
+    yield ctx, cfg, params, sched, batch
+    ctx.close()
+
+
+def test_one_epoch_local_fullsize_against_fp64_trajectory(local):
+    import torch
+    ctx, cfg, params, sched, batch = local
+    R = T * ctx.layout[0]["C"]
     dsh = [torch.from_numpy(s).cuda() for s, _ in sched]
     dpe = [torch.from_numpy(q).cuda() for _, q in sched]
     p, d, A = 0, cfg.obs_dim[0], cfg.act_dim
-    lay = ctx.layout[p]
-    batch = _batch(ctx.records_get(p), lay, d, A, ctx.adv_norm_get(p))
     shapes = O.ffn_param_shapes(d, 2 * A)
     sh, pe = sched[p]
     O64 = O.with_dtype(np.float64)
@@ -166,4 +177,57 @@ def test_one_epoch_local_fullsize_against_fp64_trajectory():
         _check_ratio(k, dg, spread, ratios)
     print("HIP / fp32-spread ratios (r03 in parentheses): " +
           ", ".join(f"{k} {v:.3f} ({R03_RATIO[k]:.2f})" for k, v in ratios.items()), flush=True)
-    ctx.close()
+
+
+@pytest.mark.timeout(600)
+def test_one_epoch_local_against_tie_following_fp64(local):
+    """Round 6: the absolute bar over the whole epoch (6,400 steps) at the bench configuration.
+
+    The bifurcation between 1,600 and 3,200 steps that the test above meets with the fp32 spread
+    is a clip decision whose fp64 margin is below fp32 resolution (DESIGN.md section 4,
+    "Near-ties", found at C4 in round 6).  Against the fp64 trajectory that takes the kernel's
+    outcome at every decision within TIE_TOL of its threshold (tests/gpu_harness.
+    tie_following_trajectory, policy 0 of the 4-policy launch), HIP must stay within
+    4 e32(H) + 2e-7 and 1e-5 at every horizon, with e32 = the numpy fp32 run's distance from
+    plain fp64, and every step's learner statistics within 1e-4 relative (+1e-6)."""
+    import torch
+    from tests.gpu_harness import tie_following_trajectory
+    ctx, cfg, params, sched, batch = local
+    p, d, A = 0, cfg.obs_dim[0], cfg.act_dim
+    shapes = O.ffn_param_shapes(d, 2 * A)
+    sh, pe = sched[p]
+    O64 = O.with_dtype(np.float64)
+    th64, _ = _run(O64, {k: v.astype(np.float64) for k, v in params[p].items()}, shapes, batch, sh, pe, HORIZONS)
+    th32, _ = _run(O, params[p], shapes, batch, sh, pe, HORIZONS)
+    theta0 = [O.pack(params[q], O.ffn_param_shapes(cfg.obs_dim[q], 2 * A)) for q in range(4)]
+    for q in range(4):
+        ctx.params_set(q, theta0[q])
+    tf, tst, ties = tie_following_trajectory(ctx, p, params[p], shapes, batch, sh, pe, 0.2, max(HORIZONS), HORIZONS,
+                                             tol=TIE_TOL)
+    flips = [t for t in ties if t[4] != t[5]]
+    print(f"\nLocal policy 0: {len(ties)} clip decisions within {TIE_TOL:g} of their threshold, {len(flips)} taken "
+          f"the other way by HIP: " + "; ".join(f"step {t[0]} {t[1]} row {t[2]} margin {t[3]:.3g}" for t in flips))
+    assert all(t[6] <= 0.1 * t[7] for t in ties), "a tie whose outcome the HIP gradient does not decide"
+    dsh = [torch.from_numpy(s).cuda() for s, _ in sched]
+    dpe = [torch.from_numpy(q).cuda() for _, q in sched]
+    fails = []
+    for H in HORIZONS:
+        for q in range(4):
+            ctx.params_set(q, theta0[q])
+            ctx.adam_set(q, np.zeros(theta0[q].size), np.zeros(theta0[q].size), 0.9, 0.999)
+        ctx.ppo_update(0xF, dsh, dpe, [0.2] * 4, max_steps=H)
+        ctx.synchronize()
+        got = ctx.params_get(p).astype(np.float64)
+        e32 = np.abs(th32[H] - th64[H]).max()
+        etf = np.abs(got - tf[H]).max()
+        print(f"H={H}: HIP - tie-following fp64 {etf:.3g} (bar {min(4 * e32 + 2e-7, 1e-5):.3g}); HIP - plain fp64 "
+              f"{np.abs(got - th64[H]).max():.3g}; numpy fp32 - plain fp64 {e32:.3g}", flush=True)
+        if not (etf <= 4 * e32 + 2e-7 and etf <= 1e-5):
+            fails.append((H, etf, e32))
+        st = ctx.ppo_stats(p, H).astype(np.float64)
+        for col, k in STAT_KEYS:
+            ref = np.array([s_[k] for s_ in tst[:H]])
+            dev = np.abs(st[:, col] - ref)
+            if not np.all(dev <= 1e-4 * np.abs(ref) + 1e-6):
+                fails.append((f"{k}@{H}", float(dev.max())))
+    assert not fails, fails
