@@ -394,7 +394,7 @@ def strict_params_check(got, model, params, shapes, batch, sh, pe, kl, steps, cf
 
 
 def tie_following_trajectory(ctx, pid, params, shapes, batch, sh, pe, kl, steps, horizons, tol=2e-5,
-                             max_combo=6, log=None):
+                             max_combo=6, log=None, model="ffn"):
     """The fp64 trajectory of the fcnet minibatch loop that takes the HIP kernel's outcome at every
     clip decision whose fp64 margin is within `tol` ("Near-ties").
 
@@ -413,7 +413,8 @@ def tie_following_trajectory(ctx, pid, params, shapes, batch, sh, pe, kl, steps,
 
     Returns (snapshots {H: fp64 theta}, per-step fp64 stats, ties), ties = one record per
     ambiguous decision: (step, kind, row, margin, fp64 outcome, HIP outcome, best / runner-up
-    gradient error).  The context's state is left arbitrary (callers reset it)."""
+    gradient error).  The context's state is left arbitrary (callers reset it).  model: "ffn" (batch
+    "obs") or "gnn" (batch "X", "node_idx")."""
     import torch
     O64 = O.with_dtype(np.float64)
     n = sum(int(np.prod(s)) for _, s in shapes)
@@ -427,10 +428,14 @@ def tie_following_trajectory(ctx, pid, params, shapes, batch, sh, pe, kl, steps,
     snaps, stats, ties = {}, [], []
     hset = set(horizons)
     cols = ("actions", "logits", "logp", "vf_preds", "adv", "vt")
+    backward = O64.gnn_backward if model == "gnn" else O64.ffn_backward
     for k in range(steps):
         rows = O.minibatch_rows(sh, pe, k // nb, k % nb)
         p = O64.unpack(theta, shapes)
-        logits, value, cache = O64.ffn_forward(p, batch["obs"][rows])
+        if model == "gnn":
+            logits, value, cache = O64.gnn_forward(p, batch["X"][rows], batch["node_idx"][rows])
+        else:
+            logits, value, cache = O64.ffn_forward(p, batch["obs"][rows])
         args = [batch[c][rows] for c in cols]
         pol_on, pol_m, vf_on, m_sq, m_in = O.ppo_branches(logits, value, args[0], args[2], args[3], args[4],
                                                           args[5])
@@ -457,7 +462,7 @@ def tie_following_trajectory(ctx, pid, params, shapes, batch, sh, pe, kl, steps,
                 for j, (kind, i, _, nat) in enumerate(amb):
                     f[kind][i] = nat if not (combo >> j) & 1 else not nat
                 dl, dv, _ = O64.ppo_loss_rows(logits, value, *args, np.float64(kl), force=f)
-                g = O64.ffn_backward(p, cache, dl, dv)
+                g = backward(p, cache, dl, dv)
                 gf = np.concatenate([g[nm].reshape(-1) for nm, _ in shapes])
                 errs.append((float(np.abs(gf - gh).max()), combo, f))
             errs.sort(key=lambda e: e[0])
@@ -470,7 +475,7 @@ def tie_following_trajectory(ctx, pid, params, shapes, batch, sh, pe, kl, steps,
                     log(f"step {k}: {kind} tie, row {i}, margin {m:.3g}, fp64 {'on' if nat else 'off'}, "
                         f"HIP {'on' if hip else 'off'} (gradient error {best:.3g}, other outcome {second:.3g})")
         dl, dv, st = O64.ppo_loss_rows(logits, value, *args, np.float64(kl), force=force)
-        g = O64.ffn_backward(p, cache, dl, dv)
+        g = backward(p, cache, dl, dv)
         clipped, gn = O64.clip_by_global_norm([g[nm] for nm, _ in shapes])
         theta = adam.apply(theta, np.concatenate([c.reshape(-1) for c in clipped]))
         st["grad_gnorm"] = float(gn)

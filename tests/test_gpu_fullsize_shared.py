@@ -369,6 +369,64 @@ def test_c5_100_steps_against_fp64(c5, c5_schedule):
     _C5_STATS100["st"] = ctx.ppo_stats(0, 100)
 
 
+C5_HORIZONS = [10, 100, 400, 1000]
+
+
+@pytest.mark.timeout(600)
+def test_c5_1000_steps_against_tie_following_fp64(c5, c5_schedule):
+    """Round 6: the one-launch GraphNet step over 1,000 sequential steps at full size (ten times
+    test_c5_100_steps_against_fp64's horizon), against the fp64 trajectory that takes the kernel's
+    outcome at clip near-ties (tests/gpu_harness.tie_following_trajectory, model "gnn"; DESIGN.md
+    section 4 "Near-ties"): within 4 e32(H) + 2e-7 and 1e-5 at every horizon, e32 = the numpy
+    fp32 run's distance from plain fp64, and every step's learner statistics within 1e-4
+    relative (+1e-6).  The numpy GraphNet costs ~25 ms per step, which sets the horizon."""
+    import torch
+    from tests.gpu_harness import tie_following_trajectory
+    ctx, cfg, params, _, rec, _ = c5
+    shapes = O.gnn_param_shapes(4)
+    theta0 = O.pack(params, shapes)
+    sh_t, pe_t = c5_schedule
+    sh, pe = sh_t.numpy(), pe_t.numpy()
+    batch = _gnn_batch(rec, ctx.layout[0], ctx.adv_norm_get(0))
+    H_MAX = max(C5_HORIZONS)
+    O64 = O.with_dtype(np.float64)
+    n = theta0.size
+
+    def run(mod, p):
+        snaps = {h: None for h in C5_HORIZONS}
+        mod.ppo_update("gnn", p, shapes, mod.Adam(n), batch, sh, pe, 0.2, {}, steps=H_MAX, snapshots=snaps)
+        return {h: np.asarray(v, np.float64) for h, v in snaps.items()}
+
+    th64 = run(O64, {k: v.astype(np.float64) for k, v in params.items()})
+    th32 = run(O, params)
+    tf, tst, ties = tie_following_trajectory(ctx, 0, params, shapes, batch, sh, pe, 0.2, H_MAX, C5_HORIZONS,
+                                             tol=TIE_TOL, model="gnn")
+    flips = [t for t in ties if t[4] != t[5]]
+    print(f"\nC5: {len(ties)} clip decisions within {TIE_TOL:g} of their threshold, {len(flips)} taken the other way "
+          f"by HIP: " + "; ".join(f"step {t[0]} {t[1]} row {t[2]} margin {t[3]:.3g}" for t in flips))
+    assert all(t[6] <= 0.1 * t[7] for t in ties), "a tie whose outcome the HIP gradient does not decide"
+    dsh, dpe = sh_t.cuda(), pe_t.cuda()
+    fails = []
+    for H in C5_HORIZONS:
+        _reset(ctx, theta0)
+        ctx.ppo_update(1, [dsh], [dpe], [0.2], max_steps=H)
+        ctx.synchronize()
+        got = ctx.params_get(0).astype(np.float64)
+        e32 = np.abs(th32[H] - th64[H]).max()
+        etf = np.abs(got - tf[H]).max()
+        print(f"C5 H={H}: HIP - tie-following fp64 {etf:.3g} (bar {min(4 * e32 + 2e-7, 1e-5):.3g}); HIP - plain "
+              f"fp64 {np.abs(got - th64[H]).max():.3g}; numpy fp32 - plain fp64 {e32:.3g}", flush=True)
+        if not (etf <= 4 * e32 + 2e-7 and etf <= 1e-5):
+            fails.append((H, etf, e32))
+        st = ctx.ppo_stats(0, H).astype(np.float64)
+        for col, k in STAT_KEYS:
+            ref = np.array([s_[k] for s_ in tst[:H]])
+            dev = np.abs(st[:, col] - ref)
+            if not np.all(dev <= 1e-4 * np.abs(ref) + 1e-6):
+                fails.append((f"{k}@{H}", float(dev.max())))
+    assert not fails, fails
+
+
 def test_c5_epoch_at_lr0_statistics_step_by_step(c5, c5_schedule):
     import torch
     from ddrl_amd import native as N
