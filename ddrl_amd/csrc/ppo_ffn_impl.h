@@ -731,6 +731,15 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
 #else
   constexpr bool NOMOM = false;
 #endif
+  // DDRL_ABL_ADAM_SPLIT: timing-only cost model (round 6) of Adam split over the two row halves
+  // -- each half updates half of the parameters, then reads its partner's half of the updated
+  // weights (results wrong)
+#ifdef DDRL_ABL_ADAM_SPLIT
+  constexpr bool ADAM_SPLIT = KSP == 2;
+#else
+  constexpr bool ADAM_SPLIT = false;
+#endif
+  const size_t gx_box_n = (size_t)GX_MAX_PAIRS * 256 * 2;   // granules per outbox
   const int wkq = ub.own_kq < 0 ? 0 : ub.own_kq;   // the half that writes back and writes the statistics
   const UpdateHyper& H = ub.h;
   const int d = U.d;
@@ -1349,7 +1358,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       // element, as the scalar form g = gt s; m += (gt s - m) c1; v += (g g - v) c2;
       // theta -= (m alpha) / (sqrt(v) + eps)
 #pragma unroll
-      for (int i = 0; i < NTS; ++i)
+      for (int i = 0; i < (ADAM_SPLIT ? (NTS + 1) / 2 : NTS); ++i)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const float2v gr = {gt[i][2 * h], gt[i][2 * h + 1]};
@@ -1373,7 +1382,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
         }
 
 #pragma unroll
-      for (int k = 0; k < NSLOT; ++k) {
+      for (int k = 0; k < (ADAM_SPLIT ? (NSLOT + 1) / 2 : NSLOT); ++k) {
         const float g = gs[k] * scale;
         ms[k] = ms[k] + (g - ms[k]) * c1;
         vs[k] = vs[k] + (g * g - vs[k]) * c2;
@@ -1394,6 +1403,20 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
         const int e = tid + NT * k;
         if (DDRL_SINK || e < nsb) lds[sp_lds[k]] = ts[k];
       }
+    }
+#endif
+#if DDRL_LX_ON
+    if constexpr (ADAM_SPLIT && LX) {
+      // the cost model's second hop: the partner's half of the updated weights (half the quads
+      // of its outbox, already valid for this step), read before sync #6
+      const int gstep = step + (int)ub.lx_base;
+      float o2[4 * ((NQ + 1) / 2)];
+      gx_get4<(NQ + 1) / 2>(lx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (gstep & 1)) * gx_box_n), lx_bit(gstep), o2,
+                             ub.err, [] {});
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4 * ((NQ + 1) / 2); ++k) acc += o2[k];
+      if (acc == 1.2345e-30f) red[127] = acc;   // keeps the loads
     }
 #endif
     b1p = b1p * H.b1;
