@@ -103,6 +103,23 @@ def pmc_mfma(key):
             "mfma_busy_frac_chip": m.get("mfma_busy_frac_chip"), "mfma_source": f"{path} ({m.get('kernel')})"}
 
 
+def parallel_mode(shared_mode, n_policies, world, force_ddp=False):
+    """How the ranks train: "single" (one process), "replicas" (independent learners on env
+    shards), "gather" (one record all-gather per iteration, the same fused
+    update over the union batch on every rank: the single-GPU algorithm exactly) or "ddp" (the
+    data-parallel learner, gradient all-reduce every SGD step; shared-policy envs only).
+    shared_mode "auto" picks gather for a shared policy and replicas otherwise; DDRL_FORCE_DDP
+    (force_ddp) names the data-parallel learner, at one rank too."""
+    if world <= 1 and not force_ddp:
+        return "single"
+    mode = shared_mode
+    if mode == "auto":
+        mode = "ddp" if force_ddp else ("gather" if n_policies == 1 else "replicas")
+    if mode == "ddp" and n_policies != 1:
+        return "replicas"
+    return mode
+
+
 def ffn_flops_per_row(d, A, H=64):
     """Algorithmic FLOPs of one minibatch row through the fused update step:
     forward (policy + value) + input-gradient backward of layers 2/head + weight gradients."""
@@ -347,12 +364,8 @@ def main():
     gnn = cfg.model_kind == N.MODEL_GNN
     # shared-policy envs on several GPUs train data-parallel (identical weights on every
     # rank); independent-policy envs are replicas (own weights per rank)
-    multi = world > 1 or force_ddp
-    mode = args.shared_mode
-    if mode == "auto":   # DDRL_FORCE_DDP names the data-parallel learner itself
-        mode = "ddp" if force_ddp else ("gather" if P == 1 else "replicas")
-    ddp = multi and P == 1 and mode == "ddp"
-    gather = multi and mode == "gather"
+    mode = parallel_mode(args.shared_mode, P, world, force_ddp)
+    ddp, gather = mode == "ddp", mode == "gather"
     if gather and args.envs % world:
         raise SystemExit("--shared-mode gather needs --envs divisible by the number of ranks")
     rng = np.random.default_rng(1234 if (ddp or gather) else 1234 + rank)

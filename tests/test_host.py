@@ -413,3 +413,21 @@ def test_glorot_gnn_init_matches_oracle_per_layer(layer):
     shapes = O.gnn_param_shapes(4, layer=layer)
     ref = O.pack(O.gnn_init(np.random.default_rng(6), 4, layer=layer), shapes)
     np.testing.assert_array_equal(glorot_gnn_flat(np.random.default_rng(6), 2, layer=layer), ref)
+
+
+def test_bench_parallel_mode_and_pmc_provenance():
+    """bench.py's choice of multi-rank mode (round 6: gather by default for a shared policy) and
+    the committed counter pass it reads its traffic / provenance figures from."""
+    import bench
+    assert bench.parallel_mode("auto", 4, 1) == "single"
+    assert bench.parallel_mode("auto", 4, 8) == "replicas"         # Local, C3: no collective
+    assert bench.parallel_mode("auto", 1, 8) == "gather"           # C4 / C5: the exact mode
+    assert bench.parallel_mode("ddp", 1, 8) == "ddp"
+    assert bench.parallel_mode("ddp", 4, 8) == "replicas"          # independent policies never all-reduce
+    assert bench.parallel_mode("gather", 4, 2) == "gather"
+    assert bench.parallel_mode("auto", 1, 1, force_ddp=True) == "ddp"
+    for key, P in (("local", 4), ("c4", 1), ("c5", 1)):
+        ns = bench.pmc_ns_per_step(key, P)
+        assert ns is not None and 5e3 < ns < 5e4, (key, ns)      # one sequential step: 5 - 50 us
+        assert bench.pmc_traffic(key, 1) > 0
+    assert bench.pmc_summary("local")[1].startswith("profiles/r06")
