@@ -431,3 +431,7 @@ def test_bench_parallel_mode_and_pmc_provenance():
         assert ns is not None and 5e3 < ns < 5e4, (key, ns)      # one sequential step: 5 - 50 us
         assert bench.pmc_traffic(key, 1) > 0
     assert bench.pmc_summary("local")[1].startswith("profiles/r06")
+    # the same recipe's kernel-trace pass, per sequential step (r06: Local 10.42 us, C5 16.83 us)
+    assert 9e3 < bench.trace_ns_per_step("local", 64000) < 12e3
+    assert 15e3 < bench.trace_ns_per_step("c5", 1) < 19e3
+    assert bench.trace_ns_per_step("c5_3launch", 1) > bench.trace_ns_per_step("c5", 1)
