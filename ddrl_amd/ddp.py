@@ -251,6 +251,21 @@ class NativeDataParallelLearner(DataParallelLearner):
         return self._kl(perms.shape[1])
 
 
+def _device_key(torch):
+    """An id of this process's current GPU that is the same in every process using that GPU (its
+    UUID or PCI bus id; device indexes differ between processes with different visible-device
+    lists), -1 without a GPU."""
+    if not torch.cuda.is_available():
+        return -1
+    props = torch.cuda.get_device_properties(torch.cuda.current_device())
+    for attr in ("uuid", "pci_bus_id"):
+        v = getattr(props, attr, None)
+        if v is not None:
+            import zlib
+            return zlib.crc32(str(v).encode()) & 0x7FFFFFFF
+    return torch.cuda.current_device()
+
+
 def peer_init(ctx, comm):
     """Peer mode: rank 0 allocates the shared outboxes (fine-grained device memory) and exports
     an IPC handle, a torch.distributed broadcast hands it to rank 1, which maps it; both attach.
@@ -262,8 +277,7 @@ def peer_init(ctx, comm):
     # path (system-scope stores over xGMI into the peer's fine-grained HBM, IPC mapping across
     # devices) has not run on hardware, so it is flagged, and PeerLearner checks the
     # ranks' weights after every update
-    dev = comm.torch.cuda.current_device() if comm.torch.cuda.is_available() else -1
-    pci = comm.all_gather_np(np.array([dev], np.int64))
+    pci = comm.all_gather_np(np.array([_device_key(comm.torch)], np.int64))
     if len({int(p[0]) for p in pci}) > 1:
         import warnings
         warnings.warn("peer mode across two GPUs is experimental: its cross-device exchange has not run on "
