@@ -54,6 +54,11 @@
 // the peer TU: atomic granules for the norm exchange and the gradient launches' pairs, quads at
 // system scope for the fused launches' partner exchange
 #define DDRL_XCHG_LXSYS (DDRL_FFN_AT == 2)
+// where the row split issues the next step's record gathers: 0 = behind the partner exchange's
+// first poll (vmcnt retires in order), 1 = right after sync #1 (round 6 A/B)
+#ifndef DDRL_GATHER_EARLY
+#define DDRL_GATHER_EARLY 0
+#endif
 // DDRL_ABL_PEER4: the timing-only cost model of a four-rank peer mode, in the
 // peer TU only: the weight-gradient K of a 32-row share and two more partners' quad reads at
 // system scope (the four-way split model of DESIGN.md section 6.2 on the peer protocol)
@@ -1036,6 +1041,11 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
     }
     STAMP(4);
     __syncthreads();                                     // #1: H1, dZ2, partials visible
+#if DDRL_GATHER_EARLY
+    // the row split's prefetch of step + 1's records, issued here: every lane read its rows of
+    // this step at the top (load_row), and the gathers now have the rest of the step to land
+    if (KSP == 2 && step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, inv_cpr_l, idxb, stg, U.R, ub.lds_bytes);
+#endif
     STAMP(5);
     const unsigned gtag = xchg_tag(ub.epoch, step);
     const int gstep = step + (int)ub.lx_base;            // outbox parity and quad tag bit
@@ -1176,14 +1186,14 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
         // 2 NQ quads of its other-parity outbox, unchecked)
         float o4[12 * NQ];
         gx_get4<NQ, 2 * NQ>(lx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (gstep & 1)) * gx_box), lbit, o4, ub.err, [&] {
-          if (step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, inv_cpr_l, idxb, stg, U.R, ub.lds_bytes);
+          if (!DDRL_GATHER_EARLY && step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, inv_cpr_l, idxb, stg, U.R, ub.lds_bytes);
         }, lx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + ((gstep + 1) & 1)) * gx_box));
 #pragma unroll
         for (int k = 0; k < 4 * NQ; ++k) o4[k] = (o4[k] + o4[4 * NQ + k]) + o4[8 * NQ + k];
 #else
         float o4[4 * NQ];
         gx_get4<NQ>(lx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (gstep & 1)) * gx_box), lbit, o4, ub.err, [&] {
-          if (step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, inv_cpr_l, idxb, stg, U.R, ub.lds_bytes);
+          if (!DDRL_GATHER_EARLY && step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, inv_cpr_l, idxb, stg, U.R, ub.lds_bytes);
         });
 #endif
 #if defined(DDRL_ABL_XCHG3)
@@ -1211,7 +1221,7 @@ __device__ __forceinline__ void update_loop(const UpdateArgs& U, const UpdateBat
       // retire first: vmcnt is in order; a re-poll then waits for them too): 13.0 -> 12.9 us
       // per step against issuing them after the exchange
       gx_get<NP>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (gstep & 1)) * gx_box), gtag, o, ub.err, [&] {
-        if (step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, inv_cpr_l, idxb, stg, U.R, ub.lds_bytes);
+        if (!DDRL_GATHER_EARLY && step + 1 < last) issue_rows<NW, ROWS>(U.rec, stride, cpr, cpr_l, inv_cpr_l, idxb, stg, U.R, ub.lds_bytes);
       });
 #else
       gx_get<NP>(gx_rsrc(ub.gx + ((gx_branch + (kq ^ 1)) * 2 + (gstep & 1)) * gx_box), gtag, o, ub.err, [] {});
