@@ -935,8 +935,14 @@ static UpdateArgs make_update(ddrl_ctx* c, int p, const int32_t* shuffle, const 
 
 int ddrl_ppo_update(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const int32_t* const* perm,
                     const float* kl, int max_steps) {
+  return ddrl_ppo_update_from(c, mask, shuffle, perm, kl, 0, max_steps);
+}
+
+int ddrl_ppo_update_from(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const int32_t* const* perm,
+                         const float* kl, int step0, int max_steps) {
   CHK_CTX(c);
   if (!shuffle || !perm || !kl) return fail("null update argument");
+  if (step0 < 0) return fail("step0 must be >= 0");
   UpdateArgs ua[DDRL_MAXP];
   int n = 0;
   for (int p = 0; p < c->cfg.n_policies; ++p) {
@@ -951,8 +957,10 @@ int ddrl_ppo_update(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const 
     ua[n] = make_update(c, p, shuffle[p], perm[p], kl[p]);
     c->kl_last[p] = kl[p];
     ua[n].max_steps = max_steps;
+    ua[n].step0 = step0;
     const int total = c->cfg.num_sgd_iter * c->pol[p].nb;
-    c->pol[p].last_steps = max_steps >= 0 ? std::min(total, max_steps) : total;
+    if (step0 > total) return fail("step0 beyond the schedule's " + std::to_string(total) + " steps");
+    c->pol[p].last_steps = max_steps >= 0 ? std::min(total - step0, max_steps) : total - step0;
     ++n;
   }
   if (n == 0) return 0;
@@ -977,9 +985,9 @@ int ddrl_ppo_update(ddrl_ctx* c, int mask, const int32_t* const* shuffle, const 
     // chunk first (stream order: after the previous run's last step), so every gradient
     // launch reads its minibatch without dependent index loads
     const size_t step_floats = (size_t)DDRL_MB * ua[0].lay.stride;
-    for (int step = 0; step < last; ++step) {
-      const int k = step % CH;
-      if (k == 0) launch_gnn_gather(c->stream, ua[0], step, std::min(CH, last - step), c->gnn.chunk);
+    for (int step = step0; step < step0 + last; ++step) {
+      const int k = (step - step0) % CH;
+      if (k == 0) launch_gnn_gather(c->stream, ua[0], step, std::min(CH, step0 + last - step), c->gnn.chunk);
       launch_step_gnn(c->stream, ua[0], h, step, 128, 1.f / c->cfg.sgd_minibatch_size, c->gnn,
                       c->gnn.chunk + k * step_floats, c->cfg.gnn_layer);
     }

@@ -1562,8 +1562,24 @@ void DDRL_FFN_LAUNCH(hipStream_t s, const UpdateArgs* ua, const UpdateHyper& h, 
   // (peer mode: gx is shared with the peer context's launch, which may be running; it is cleared
   // when the peers attach, ddrl_peer_attach, and the quads' tag bits follow the pair's global
   // step count, lx_base, so a value left from an earlier launch never matches)
-  if (own_kq < 0 && (ub.epoch == 1 || (lx && DDRL_LX_ON)))
-    (void)hipMemsetAsync(gx, 0, gx_bytes(DDRL_MAXP), s);
+  if (own_kq < 0 && (ub.epoch == 1 || (lx && DDRL_LX_ON))) {
+    // A launch resumed at schedule step s0 (ddrl_ppo_update_from) keeps the quads' tag bits of
+    // the global step, so the outbox of each parity must start with the complement of the bit
+    // of its first use, s0 or s0 + 1: zero words would pass a first bit of 0.  One byte pattern
+    // per parity (0x00: LSB 0, 0x01: LSB 1; the pairs' epoch tags never equal 0x01010101).
+    const int s0 = ua[0].step0;
+    const unsigned b0 = (((unsigned)s0 >> 1) & 1u) ^ 1u, b1 = (((unsigned)(s0 + 1) >> 1) & 1u) ^ 1u;
+    if (!(lx && DDRL_LX_ON) || (b0 && b1)) {
+      (void)hipMemsetAsync(gx, 0, gx_bytes(DDRL_MAXP), s);
+    } else {
+      const size_t box = sizeof(unsigned long long) * (size_t)GX_MAX_PAIRS * 256 * 2;
+      const size_t nbox = gx_bytes(DDRL_MAXP) / box;   // box index = 2 * (branch slot) + parity
+      for (int q = 0; q < 2; ++q) {
+        const unsigned first_bit = (s0 & 1) == q ? b0 : b1;
+        (void)hipMemset2DAsync(reinterpret_cast<char*>(gx) + q * box, 2 * box, first_bit ? 0 : 1, box, nbox / 2, s);
+      }
+    }
+  }
   if (cup)   // "cup": one shared leg policy, A = 2, d <= 20 (capi validate)
     launch_update_t<2, 5, true>(s, ub, h.P, stride, ksp, lx);
   else

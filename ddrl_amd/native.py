@@ -78,6 +78,7 @@ _SIGS = {
     "ddrl_env_step_host": ([VP, C.c_int, VP, VP, VP, VP], C.c_int),
     "ddrl_gae": ([VP], C.c_int),
     "ddrl_ppo_update": ([VP, C.c_int, C.POINTER(VP), C.POINTER(VP), C.POINTER(f32), C.c_int], C.c_int),
+    "ddrl_ppo_update_from": ([VP, C.c_int, C.POINTER(VP), C.POINTER(VP), C.POINTER(f32), C.c_int, C.c_int], C.c_int),
     "ddrl_ppo_stats": ([VP, C.c_int, VP, C.c_size_t], C.c_int),
     "ddrl_ppo_stats_range": ([VP, C.c_int, C.c_size_t, C.c_size_t, VP], C.c_int),
     "ddrl_ppo_grad": ([VP, C.c_int, VP, C.c_int, f32, VP, C.c_int], C.c_int),
@@ -371,12 +372,17 @@ class Context:
         _ck(self.lib.ddrl_gae(self.h))
 
     # ---- learner ----
-    def ppo_update(self, mask, shuffles, perms, kl_coeffs, max_steps=-1):
+    def ppo_update(self, mask, shuffles, perms, kl_coeffs, max_steps=-1, step0=0):
+        """The fused minibatch SGD (ddrl_ppo_update); step0 > 0 resumes the schedule at that step
+        (ddrl_ppo_update_from), bit-identical to the same steps of one uninterrupted launch."""
         P = self.cfg.n_policies
         sh = (VP * MAX_P)(*[_ptr(shuffles[p]) if shuffles[p] is not None else None for p in range(P)])
         pe = (VP * MAX_P)(*[_ptr(perms[p]) if perms[p] is not None else None for p in range(P)])
         kl = (f32 * MAX_P)(*[float(k) for k in kl_coeffs])
-        _ck(self.lib.ddrl_ppo_update(self.h, mask, sh, pe, kl, max_steps))
+        if step0:
+            _ck(self.lib.ddrl_ppo_update_from(self.h, mask, sh, pe, kl, step0, max_steps))
+        else:
+            _ck(self.lib.ddrl_ppo_update(self.h, mask, sh, pe, kl, max_steps))
 
     def ppo_stats(self, pid, n_steps, first=0):
         """Learner statistics rows [first, first + n_steps) of the last update (8 floats each)."""

@@ -224,6 +224,13 @@ int ddrl_adv_sums_get(ddrl_ctx* ctx, int pid, double* host3);
  * All policies in the mask run concurrently (one persistent workgroup each). */
 int ddrl_ppo_update(ddrl_ctx* ctx, int pid_mask, const int32_t* const* shuffle_dev,
                     const int32_t* const* perm_dev, const float* kl_coeff, int max_steps);
+/* The same update resumed at minibatch step step0 of the schedule (step0 = e * nb + b), from the
+ * weights, Adam state and beta powers the context holds (e.g. restored from a mid-update
+ * checkpoint): bit-identical to steps step0 .. of one uninterrupted ddrl_ppo_update (round 6; the
+ * fused exchange's tag bits follow the schedule step).  Learner statistics land in rows step0 ..;
+ * max_steps counts from step0.  ddrl_ppo_update is ddrl_ppo_update_from(…, 0, max_steps). */
+int ddrl_ppo_update_from(ddrl_ctx* ctx, int pid_mask, const int32_t* const* shuffle_dev,
+                         const int32_t* const* perm_dev, const float* kl_coeff, int step0, int max_steps);
 /* Per-minibatch learner stats of the last update: n_steps x 8 floats
  * {total_loss, policy_loss, vf_loss, kl, entropy, vf_explained_var, grad_gnorm, clip_scale}. */
 int ddrl_ppo_stats(ddrl_ctx* ctx, int pid, float* host, size_t n_steps);
