@@ -393,42 +393,116 @@ def strict_params_check(got, model, params, shapes, batch, sh, pe, kl, steps, cf
     return n_over, n_ex, n
 
 
-def tie_following_trajectory(ctx, pid, params, shapes, batch, sh, pe, kl, steps, horizons, tol=2e-5,
-                             max_combo=6, log=None, model="ffn"):
-    """The fp64 trajectory of the fcnet minibatch loop that takes the HIP kernel's outcome at every
-    clip decision whose fp64 margin is within `tol` ("Near-ties").
+class HipLockstep:
+    """The HIP trajectory of policy `pid`, one step at a time (ddrl_ppo_update_from: bit-identical
+    to one uninterrupted launch), with the HIP gradient of a minibatch from its current state
+    (ddrl_ppo_grad)."""
+
+    def __init__(self, ctx, pid, theta0, sh, pe, kl):
+        import torch
+        self.ctx, self.pid, self.kl = ctx, pid, kl
+        P = ctx.cfg.n_policies
+        self.P = P
+        self.dsh = [torch.from_numpy(np.ascontiguousarray(sh)).cuda() if q == pid else None for q in range(P)]
+        self.dpe = [torch.from_numpy(np.ascontiguousarray(pe)).cuda() if q == pid else None for q in range(P)]
+        n = theta0.size
+        self.gbuf = torch.zeros(n, device="cuda")
+        self.snaps = {}
+        ctx.params_set(pid, theta0)
+        ctx.adam_set(pid, np.zeros(n, np.float32), np.zeros(n, np.float32), 0.9, 0.999)
+
+    def grad(self, rows):
+        import torch
+        r = torch.from_numpy(np.ascontiguousarray(rows)).cuda()
+        self.ctx.ppo_grad(self.pid, r, rows.size, self.kl, self.gbuf)
+        self.ctx.synchronize()
+        return self.gbuf.cpu().numpy().astype(np.float64)
+
+    def step(self, k):
+        self.ctx.ppo_update(1 << self.pid, self.dsh, self.dpe, [self.kl] * self.P, max_steps=1, step0=k)
+
+    def theta(self):
+        self.ctx.synchronize()
+        return self.ctx.params_get(self.pid).astype(np.float64)
+
+
+class NumpyLockstep:
+    """The numpy fp32 oracle's trajectory, one step at a time, with its gradient of a minibatch
+    from its current state: an fp32 implementation whose tie outcomes are numpy's."""
+
+    def __init__(self, params, shapes, batch, sh, pe, kl, model="ffn"):
+        self.shapes, self.batch, self.sh, self.pe, self.kl, self.model = shapes, batch, sh, pe, kl, model
+        self.th = O.pack(params, shapes)
+        self.adam = O.Adam(self.th.size)
+        self.snaps = {}
+
+    def _fwd_bwd(self, rows):
+        b, p = self.batch, O.unpack(self.th, self.shapes)
+        if self.model == "gnn":
+            logits, value, cache = O.gnn_forward(p, b["X"][rows], b["node_idx"][rows])
+        else:
+            logits, value, cache = O.ffn_forward(p, b["obs"][rows])
+        dl, dv, _ = O.ppo_loss_rows(logits, value, b["actions"][rows], b["logits"][rows], b["logp"][rows],
+                                    b["vf_preds"][rows], b["adv"][rows], b["vt"][rows], np.float32(self.kl))
+        g = (O.gnn_backward if self.model == "gnn" else O.ffn_backward)(p, cache, dl, dv)
+        return [g[nm] for nm, _ in self.shapes]
+
+    def grad(self, rows):
+        return np.concatenate([g.reshape(-1) for g in self._fwd_bwd(rows)]).astype(np.float64)
+
+    def step(self, k):
+        nb = self.pe.shape[1]
+        rows = O.minibatch_rows(self.sh, self.pe, k // nb, k % nb)
+        clipped, _ = O.clip_by_global_norm(self._fwd_bwd(rows))
+        self.th = self.adam.apply(self.th, np.concatenate([c.reshape(-1) for c in clipped]))
+
+    def theta(self):
+        return np.asarray(self.th, np.float64)
+
+
+def tie_following_trajectory(ctx, pid, params, shapes, batch, sh, pe, kl, steps, horizons, tol=None,
+                             max_flips=8, log=None, model="ffn", detect=2e-4, impl=None):
+    """The fp64 trajectory of the minibatch loop that takes an fp32 implementation's outcome at
+    every clip decision it took the other way ("Near-ties").
 
     PPO's loss has two clip decisions per row, each a discontinuity of the gradient: the
     surrogate passes gradient or not (ratio against 1 +- clip) and the value term passes gradient
     or not (|V - vf_old| against vf_clip, and (V - vt)^2 against the clipped square).  When a
     decision's deciding quantity lies within fp32 resolution of its threshold, its outcome is set
     by the implementation's rounding -- TF's, numpy's, the HIP kernel's alike -- and a flip changes
-    that step's gradient by a finite amount; the trajectories bifurcate there.  This loop runs
-    the fp64 algorithm and, at every step with an ambiguous decision (relative margin < tol,
-    oracle.ppo_branches), asks the HIP kernel which way it went: the context is reset to the
-    starting state, a fused launch runs the first k steps (the HIP trajectory's state), and
-    ddrl_ppo_grad returns the HIP gradient of step k's minibatch; the fp64 gradient is formed for
-    every combination of the ambiguous decisions and the closest one is taken.  Everything else
-    is fp64 arithmetic of the unmodified algorithm.
+    that step's gradient by a finite amount; the trajectories bifurcate there.
 
-    Returns (snapshots {H: fp64 theta}, per-step fp64 stats, ties), ties = one record per
-    ambiguous decision: (step, kind, row, margin, fp64 outcome, HIP outcome, best / runner-up
-    gradient error).  The context's state is left arbitrary (callers reset it).  model: "ffn" (batch
-    "obs") or "gnn" (batch "X", "node_idx")."""
-    import torch
+    Lockstep (round 6): the implementation (`impl`: HipLockstep over `ctx` by default, or
+    NumpyLockstep) walks its own trajectory one step at a time, and at every step returns its
+    gradient of that step's minibatch from its own state.  The fp64 algorithm runs beside it from
+    its own state; where the two gradients differ by more than `detect` (relative to the largest
+    fp64 entry) the rows whose decisions flipped are found greedily among the rows of smallest
+    margin (oracle.ppo_branches), each flip kept only if it halves the difference, and the fp64
+    step takes the implementation's outcomes (oracle.ppo_loss_rows(force=...)).  No margin
+    tolerance is involved: a flip of any margin is seen.  Everything else is the unmodified fp64
+    algorithm.  (`tol` is accepted for the older signature and unused.)
+
+    Returns (snapshots {H: fp64 theta}, per-step fp64 stats, ties) and leaves the implementation's
+    own parameters at each horizon in impl.snaps; ties =
+    one record per followed decision: (step, kind, row, margin, fp64 outcome, implementation's
+    outcome, gradient difference with the implementation's outcome, with fp64's), differences
+    relative to max |g_fp64|.  model: "ffn" (batch "obs") or "gnn" (batch "X", "node_idx")."""
     O64 = O.with_dtype(np.float64)
-    n = sum(int(np.prod(s)) for _, s in shapes)
+    n = sum(int(np.prod(s_)) for _, s_ in shapes)
     theta0 = O.pack(params, shapes)
+    if impl is None:
+        impl = HipLockstep(ctx, pid, theta0, sh, pe, kl)
     theta = theta0.astype(np.float64)
     adam = O64.Adam(n)
     epochs, nb = pe.shape
-    dsh = torch.from_numpy(np.ascontiguousarray(sh)).cuda()
-    dpe = torch.from_numpy(np.ascontiguousarray(pe)).cuda()
-    gbuf = torch.zeros(n, device="cuda")
     snaps, stats, ties = {}, [], []
     hset = set(horizons)
     cols = ("actions", "logits", "logp", "vf_preds", "adv", "vt")
     backward = O64.gnn_backward if model == "gnn" else O64.ffn_backward
+
+    def flat(g):
+        return np.concatenate([g[nm].reshape(-1) for nm, _ in shapes])
+
     for k in range(steps):
         rows = O.minibatch_rows(sh, pe, k // nb, k % nb)
         p = O64.unpack(theta, shapes)
@@ -437,49 +511,61 @@ def tie_following_trajectory(ctx, pid, params, shapes, batch, sh, pe, kl, steps,
         else:
             logits, value, cache = O64.ffn_forward(p, batch["obs"][rows])
         args = [batch[c][rows] for c in cols]
-        pol_on, pol_m, vf_on, m_sq, m_in = O.ppo_branches(logits, value, args[0], args[2], args[3], args[4],
-                                                          args[5])
-        amb = [("pol", int(i), float(pol_m[i]), bool(pol_on[i])) for i in np.flatnonzero(np.abs(pol_m) < tol)]
-        vamb = ((np.abs(m_sq) < tol) & ~(m_in > tol)) | ((np.abs(m_in) < tol) & ~(m_sq > tol))
-        amb += [("vf", int(i), float(m_sq[i] if abs(m_sq[i]) < abs(m_in[i]) else m_in[i]), bool(vf_on[i]))
-                for i in np.flatnonzero(vamb)]
-        force = None
-        if amb:
-            assert len(amb) <= max_combo, ("too many ambiguous decisions in one step", k, amb)
-            ctx.params_set(pid, theta0)
-            ctx.adam_set(pid, np.zeros(n, np.float32), np.zeros(n, np.float32), 0.9, 0.999)
-            if k > 0:
-                P = ctx.cfg.n_policies
-                ctx.ppo_update(1 << pid, [dsh if q == pid else None for q in range(P)],
-                               [dpe if q == pid else None for q in range(P)], [kl] * P, max_steps=k)
-            r = torch.from_numpy(np.ascontiguousarray(rows)).cuda()
-            ctx.ppo_grad(pid, r, rows.size, kl, gbuf)
-            ctx.synchronize()
-            gh = gbuf.cpu().numpy().astype(np.float64)
-            errs = []
-            for combo in range(1 << len(amb)):
-                f = {"pol": {}, "vf": {}}
-                for j, (kind, i, _, nat) in enumerate(amb):
-                    f[kind][i] = nat if not (combo >> j) & 1 else not nat
-                dl, dv, _ = O64.ppo_loss_rows(logits, value, *args, np.float64(kl), force=f)
-                g = backward(p, cache, dl, dv)
-                gf = np.concatenate([g[nm].reshape(-1) for nm, _ in shapes])
-                errs.append((float(np.abs(gf - gh).max()), combo, f))
-            errs.sort(key=lambda e: e[0])
-            best, combo, force = errs[0]
-            second = errs[1][0]
-            for j, (kind, i, m, nat) in enumerate(amb):
-                hip = nat if not (combo >> j) & 1 else not nat
-                ties.append((k, kind, i, m, nat, hip, best, second))
-                if log:
-                    log(f"step {k}: {kind} tie, row {i}, margin {m:.3g}, fp64 {'on' if nat else 'off'}, "
-                        f"HIP {'on' if hip else 'off'} (gradient error {best:.3g}, other outcome {second:.3g})")
-        dl, dv, st = O64.ppo_loss_rows(logits, value, *args, np.float64(kl), force=force)
+        dl, dv, st = O64.ppo_loss_rows(logits, value, *args, np.float64(kl))
+        g_nat = flat(backward(p, cache, dl, dv))
+        gh = impl.grad(rows)
+        scale = max(np.abs(g_nat).max(), 1e-30)
+        err_nat = np.abs(gh - g_nat).max() / scale
+        if err_nat > detect:
+            pol_on, pol_m, vf_on, m_sq, m_in = O.ppo_branches(logits, value, args[0], args[2], args[3], args[4],
+                                                              args[5])
+            # the value decision's margin: the quantity that decides it (inside the clip: |dv|
+            # against vf_clip; outside: the two squares)
+            vm = np.where(m_in > 0, m_in, np.minimum(np.abs(m_in), np.abs(m_sq)))
+            cand = sorted([(abs(float(pol_m[i])), "pol", int(i), float(pol_m[i]), bool(pol_on[i]))
+                           for i in range(rows.size)] +
+                          [(abs(float(vm[i])), "vf", int(i), float(vm[i]), bool(vf_on[i]))
+                           for i in range(rows.size)])[:max_flips]
+            f = {"pol": {}, "vf": {}}
+            cur, chosen = err_nat, {}
+            for _ in range(max_flips):
+                best = None
+                for _, kind, i, m, nat in cand:
+                    if i in f[kind]:
+                        continue
+                    f2 = {"pol": dict(f["pol"]), "vf": dict(f["vf"])}
+                    f2[kind][i] = not nat
+                    d2, v2, _ = O64.ppo_loss_rows(logits, value, *args, np.float64(kl), force=f2)
+                    e2 = np.abs(gh - flat(backward(p, cache, d2, v2))).max() / scale
+                    if best is None or e2 < best[0]:
+                        best = (e2, kind, i, m, nat)
+                if best is None or best[0] > 0.5 * cur:
+                    break
+                cur = best[0]
+                f[best[1]][best[2]] = not best[4]
+                chosen[(best[1], best[2])] = (best[3], best[4])
+                if cur <= detect:
+                    break
+            if chosen:
+                for (kind, i), (m, nat) in chosen.items():
+                    # the runner-up: this decision toggled back to fp64's outcome
+                    f3 = {"pol": dict(f["pol"]), "vf": dict(f["vf"])}
+                    f3[kind][i] = nat
+                    d3, v3, _ = O64.ppo_loss_rows(logits, value, *args, np.float64(kl), force=f3)
+                    e3 = np.abs(gh - flat(backward(p, cache, d3, v3))).max() / scale
+                    ties.append((k, kind, i, m, nat, not nat, cur, e3))
+                    if log:
+                        log(f"step {k}: {kind} clip of row {i}, fp64 margin {m:.3g}, fp64 {'on' if nat else 'off'}, "
+                            f"implementation {'off' if nat else 'on'} (relative gradient difference {cur:.3g}; "
+                            f"{e3:.3g} with fp64's outcome)")
+                dl, dv, st = O64.ppo_loss_rows(logits, value, *args, np.float64(kl), force=f)
         g = backward(p, cache, dl, dv)
         clipped, gn = O64.clip_by_global_norm([g[nm] for nm, _ in shapes])
         theta = adam.apply(theta, np.concatenate([c.reshape(-1) for c in clipped]))
         st["grad_gnorm"] = float(gn)
         stats.append(st)
+        impl.step(k)
         if k + 1 in hset:
             snaps[k + 1] = theta.copy()
+            impl.snaps[k + 1] = impl.theta()
     return snaps, stats, ties
