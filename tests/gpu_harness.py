@@ -461,7 +461,7 @@ class NumpyLockstep:
 
 
 def tie_following_trajectory(ctx, pid, params, shapes, batch, sh, pe, kl, steps, horizons, tol=None,
-                             max_flips=8, log=None, model="ffn", detect=2e-4, impl=None):
+                             max_flips=8, log=None, model="ffn", detect=2e-4, impl=None, pool=48, missed=None):
     """The fp64 trajectory of the minibatch loop that takes an fp32 implementation's outcome at
     every clip decision it took the other way ("Near-ties").
 
@@ -476,11 +476,13 @@ def tie_following_trajectory(ctx, pid, params, shapes, batch, sh, pe, kl, steps,
     NumpyLockstep) walks its own trajectory one step at a time, and at every step returns its
     gradient of that step's minibatch from its own state.  The fp64 algorithm runs beside it from
     its own state; where the two gradients differ by more than `detect` (relative to the largest
-    fp64 entry) the rows whose decisions flipped are found greedily among the rows of smallest
-    margin (oracle.ppo_branches), each flip kept only if it halves the difference, and the fp64
-    step takes the implementation's outcomes (oracle.ppo_loss_rows(force=...)).  No margin
-    tolerance is involved: a flip of any margin is seen.  Everything else is the unmodified fp64
-    algorithm.  (`tol` is accepted for the older signature and unused.)
+    fp64 entry) the decisions that flipped are found greedily among the `pool` decisions of
+    smallest margin (oracle.ppo_branches), each flip kept only if it halves the difference, and
+    the fp64 step takes the implementation's outcomes (oracle.ppo_loss_rows(force=...)).  No
+    margin tolerance is involved: a flip of any margin within the pool is seen.  A step whose
+    difference stays above `detect` after the search is appended to `missed` (step, difference
+    before, after) when a list is given.  Everything else is the unmodified fp64 algorithm.
+    (`tol` is accepted for the older signature and unused.)
 
     Returns (snapshots {H: fp64 theta}, per-step fp64 stats, ties) and leaves the implementation's
     own parameters at each horizon in impl.snaps; ties =
@@ -525,7 +527,7 @@ def tie_following_trajectory(ctx, pid, params, shapes, batch, sh, pe, kl, steps,
             cand = sorted([(abs(float(pol_m[i])), "pol", int(i), float(pol_m[i]), bool(pol_on[i]))
                            for i in range(rows.size)] +
                           [(abs(float(vm[i])), "vf", int(i), float(vm[i]), bool(vf_on[i]))
-                           for i in range(rows.size)])[:max_flips]
+                           for i in range(rows.size)])[:pool]
             f = {"pol": {}, "vf": {}}
             cur, chosen = err_nat, {}
             for _ in range(max_flips):
@@ -546,6 +548,11 @@ def tie_following_trajectory(ctx, pid, params, shapes, batch, sh, pe, kl, steps,
                 chosen[(best[1], best[2])] = (best[3], best[4])
                 if cur <= detect:
                     break
+            if cur > detect:
+                if missed is not None:
+                    missed.append((k, float(err_nat), float(cur)))
+                if log:
+                    log(f"step {k}: gradient difference {err_nat:.3g} ({cur:.3g} after the flips found) not explained")
             if chosen:
                 for (kind, i), (m, nat) in chosen.items():
                     # the runner-up: this decision toggled back to fp64's outcome

@@ -254,14 +254,18 @@ def test_c4_quarter_epoch_against_tie_following_fp64(c4):
               _run(O, params, shapes, batch, _row_order_variant(sh, 90), pe, HORIZONS),
               _run(O, _ulp_variant(params, 200), shapes, batch, sh, pe, HORIZONS),
               _run(_fast_tanh_oracle(), params, shapes, batch, sh, pe, HORIZONS)]
-    tf, tst, ties = tie_following_trajectory(ctx, 0, params, shapes, batch, sh, pe, 0.2, H_MAX, HORIZONS)
-    print(f"\nC4 tie-following fp64 trajectory: {len(ties)} clip decisions taken the other way by HIP:")
+    missed = []
+    tf, tst, ties = tie_following_trajectory(ctx, 0, params, shapes, batch, sh, pe, 0.2, H_MAX, HORIZONS,
+                                             missed=missed)
+    print(f"\nC4 tie-following fp64 trajectory: {len(ties)} clip decisions taken the other way by HIP; "
+          f"{len(missed)} steps whose gradient difference no flip explains {missed[:5]}:")
     for k, kind, i, m, nat, hip, best, second in ties:
         print(f"  step {k}: {'value' if kind == 'vf' else 'surrogate'} clip of minibatch row {i}, fp64 margin "
               f"{m:.3g}, fp64 {'passes' if nat else 'clips'}, HIP {'passes' if hip else 'clips'} (HIP gradient vs "
               f"fp64 with HIP's outcome {best:.3g}, with fp64's {second:.3g})")
     fails = []
-    # every decision was read unambiguously off the HIP gradient
+    # every departure of the HIP gradient from fp64 is a flipped decision, read unambiguously
+    fails += [("unexplained step", m) for m in missed]
     for t in ties:
         if not t[6] <= 0.5 * t[7]:
             fails.append(("undecided tie", t))
@@ -393,10 +397,13 @@ def test_c5_1000_steps_against_tie_following_fp64(c5, c5_schedule):
 
     th64 = run(O64, {k: v.astype(np.float64) for k, v in params.items()})
     th32 = run(O, params)
+    missed = []
     tf, tst, ties = tie_following_trajectory(ctx, 0, params, shapes, batch, sh, pe, 0.2, H_MAX, C5_HORIZONS,
-                                             model="gnn")
+                                             model="gnn", missed=missed)
     print(f"\nC5: {len(ties)} clip decisions taken the other way by HIP: " +
-          "; ".join(f"step {t[0]} {t[1]} row {t[2]} margin {t[3]:.3g}" for t in ties))
+          "; ".join(f"step {t[0]} {t[1]} row {t[2]} margin {t[3]:.3g}" for t in ties) +
+          f"; {len(missed)} steps whose gradient difference no flip explains {missed[:5]}")
+    assert not missed, missed[:5]
     assert all(t[6] <= 0.5 * t[7] for t in ties), "a tie whose outcome the HIP gradient does not decide"
     dsh, dpe = sh_t.cuda(), pe_t.cuda()
     fails = []

@@ -189,7 +189,11 @@ def test_one_epoch_local_against_tie_following_fp64(local):
     a time (ddrl_ppo_update_from) beside the fp64 one and takes HIP's outcome at every decision it
     took the other way.  The numpy fp32 oracle is measured the same way -- its own lockstep
     against the fp64 trajectory that follows numpy's outcomes -- which gives e32(H), the rounding
-    drift of an fp32 implementation with the bifurcations taken out.  Bar, per policy and horizon:
+    drift of an fp32 implementation with the bifurcations taken out.  Through 3,200 steps every
+    step whose HIP gradient departs from fp64's by more than the search threshold must be explained
+    by flipped decisions (late in the epoch both implementations drift smoothly, gradient
+    differences of 2e-4 - 6e-4 that no flip explains, and those steps are counted and printed).
+    Bar, per policy and horizon:
     |HIP - fp64 following HIP| <= 4 e32(H) + 2e-7; within 1e-5 absolute through H = 3,200 for every
     policy (the north_star tolerance); every step's learner statistics within 1e-4 relative
     (+1e-6) of the tie-following fp64 ones; and the one-step-at-a-time HIP walk bit-identical to
@@ -205,17 +209,24 @@ def test_one_epoch_local_against_tie_following_fp64(local):
         batch = batch0 if q == 0 else _batch(ctx.records_get(q), ctx.layout[q], cfg.obs_dim[q], A, ctx.adv_norm_get(q))
         sh, pe = sched[q]
         npl = NumpyLockstep(params[q], shapes[q], batch, sh, pe, 0.2)
+        missed32, missed = [], []
         tf32, _, ties32 = tie_following_trajectory(None, q, params[q], shapes[q], batch, sh, pe, 0.2, max(HORIZONS),
-                                                   HORIZONS, impl=npl)
+                                                   HORIZONS, impl=npl, missed=missed32)
         for r in range(4):
             ctx.params_set(r, theta0[r])
         hip = HipLockstep(ctx, q, theta0[q], sh, pe, 0.2)
         tf, tst, ties = tie_following_trajectory(ctx, q, params[q], shapes[q], batch, sh, pe, 0.2, max(HORIZONS),
-                                                 HORIZONS, impl=hip)
+                                                 HORIZONS, impl=hip, missed=missed)
         print(f"\nLocal policy {q}: HIP took {len(ties)} clip decisions the other way from fp64: " +
               "; ".join(f"step {t[0]} {t[1]} row {t[2]} margin {t[3]:.3g}" for t in ties) +
               f"; numpy fp32 took {len(ties32)}: " +
-              "; ".join(f"step {t[0]} {t[1]} row {t[2]} margin {t[3]:.3g}" for t in ties32), flush=True)
+              "; ".join(f"step {t[0]} {t[1]} row {t[2]} margin {t[3]:.3g}" for t in ties32) +
+              f"; steps whose gradient difference no flip explains: HIP {len(missed)} (from step "
+              f"{missed[0][0] if missed else '-'}, at most {max([m[1] for m in missed], default=0):.3g}), numpy "
+              f"{len(missed32)} (from step {missed32[0][0] if missed32 else '-'}, at most "
+              f"{max([m[1] for m in missed32], default=0):.3g})", flush=True)
+        # every departure of HIP from fp64 through the absolute-bar range is a flipped clip decision
+        assert all(m[0] >= 3200 for m in missed), (q, missed[:5])
         assert all(t[6] <= 0.5 * t[7] for t in ties), (q, "a tie whose outcome the HIP gradient does not decide")
         e32 = {H: np.abs(npl.snaps[H] - tf32[H]).max() for H in HORIZONS}
         refs.append((tf, tst, e32, hip.snaps))
