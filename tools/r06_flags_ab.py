@@ -12,6 +12,9 @@ VARIANTS = {
     "trackers": ["-mllvm", "-amdgpu-use-amdgpu-trackers"],
     "noclusterrp": ["-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule"],
     "maxilp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+    # no SLP auto-packing of scalar f32 code into v_pk_* (MI355X_MICROARCH.md: packed f32 VALU
+    # beside MFMAs is an anti-lever); Adam's explicit float2 ops stay packed
+    "noslp": ["-fno-slp-vectorize"],
 }
 
 
