@@ -1,0 +1,80 @@
+"""r06 diagnostic: the Local tie-following comparison of tests/test_gpu_longhorizon.py carried past
+one epoch, for one policy (GPU box, repo root):
+
+    python tools/r06_long_walk.py [policy] [steps]      # default policy 0, 64,000 steps (the iteration)
+
+The bench configuration (4096 envs x T = 200, the test's seeds), policy `policy`: HIP walked one
+step at a time (ddrl_ppo_update_from) beside the fp64 trajectory that follows its clip outcomes,
+and the numpy fp32 oracle walked the same way beside its own; distances printed at every horizon
+and progress every 2,000 steps."""
+import os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+
+
+def main(q=0, steps=64000):
+    import torch
+    from oracle import ddrl_oracle as O
+    from ddrl_amd.synthetic import SyntheticRollout
+    from tests.gpu_harness import HipLockstep, NumpyLockstep, init_params, make_ctx, tie_following_trajectory
+    from tests.test_gpu_longhorizon import N_ENVS, T, _batch
+    ctx, cfg, _ = make_ctx("QuantrupedMultiEnv_Local", N_ENVS, T)
+    params = init_params(ctx, cfg, 21, head_scale=1.0)
+    syn = SyntheticRollout(N_ENVS, T, cfg.obs_full_dim, cfg.n_agents, cfg.act_dim, "cuda:0", seed=3)
+    ctx.observe(syn.obs[0])
+    ctx.rollout_fragment(syn.obs, syn.eps, syn.fw, syn.cfrc, syn.dones_for_fragment(), syn.actions)
+    ctx.gae()
+    ctx.synchronize()
+    del syn
+    R = T * ctx.layout[0]["C"]
+    sched = [O.sgd_schedule(np.random.default_rng(40 + p), R, 128, 10) for p in range(4)]
+    A = cfg.act_dim
+    shapes = O.ffn_param_shapes(cfg.obs_dim[q], 2 * A)
+    batch = _batch(ctx.records_get(q), ctx.layout[q], cfg.obs_dim[q], A, ctx.adv_norm_get(q))
+    sh, pe = sched[q]
+    horizons = sorted({h for h in (1600, 3200, 6400, 12800, 19200, 25600, 32000, 44800, 64000) if h <= steps} | {steps})
+    t0 = time.time()
+
+    class Progress:
+        """Wraps an implementation: a progress line every 2,000 steps (the box's hang detector)."""
+        def __init__(self, impl, tag):
+            self.impl, self.tag = impl, tag
+            self.snaps = impl.snaps
+
+        def grad(self, rows):
+            return self.impl.grad(rows)
+
+        def step(self, k):
+            self.impl.step(k)
+            if (k + 1) % 2000 == 0:
+                print(f"{self.tag}: step {k + 1} ({time.time() - t0:.0f} s)", flush=True)
+
+        def theta(self):
+            return self.impl.theta()
+
+    # past the first epoch most steps differ by more than the search threshold with no flip to
+    # explain them (smooth drift): a small search keeps the walk affordable
+    search = dict(pool=16, max_flips=2)
+    npl = NumpyLockstep(params[q], shapes, batch, sh, pe, 0.2)
+    m32 = []
+    tf32, _, ties32 = tie_following_trajectory(None, q, params[q], shapes, batch, sh, pe, 0.2, steps, horizons,
+                                               impl=Progress(npl, "numpy"), missed=m32, **search)
+    for h in horizons:
+        print(f"numpy H={h}: |numpy fp32 - fp64 following numpy| {np.abs(npl.snaps[h] - tf32[h]).max():.3g}", flush=True)
+    hip = HipLockstep(ctx, q, O.pack(params[q], shapes), sh, pe, 0.2)
+    mh = []
+    tf, _, ties = tie_following_trajectory(ctx, q, params[q], shapes, batch, sh, pe, 0.2, steps, horizons,
+                                           impl=Progress(hip, "HIP"), missed=mh, **search)
+    print(f"policy {q}: flips HIP {len(ties)}, numpy {len(ties32)}; unexplained steps HIP {len(mh)} "
+          f"(first {mh[0][0] if mh else '-'}), numpy {len(m32)} (first {m32[0][0] if m32 else '-'})", flush=True)
+    for h in horizons:
+        eh = np.abs(hip.snaps[h] - tf[h]).max()
+        en = np.abs(npl.snaps[h] - tf32[h]).max()
+        moved = np.abs(tf[h] - O.pack(params[q], shapes)).max()
+        print(f"H={h}: |HIP - fp64 following HIP| {eh:.3g}, |numpy fp32 - fp64 following numpy| {en:.3g}, "
+              f"HIP / numpy {eh / en if en else float('inf'):.2f}; max |theta - theta0| {moved:.3g}", flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main(*(int(a) for a in sys.argv[1:3]))
