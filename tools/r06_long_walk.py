@@ -2,6 +2,7 @@
 one epoch, for one policy (GPU box, repo root):
 
     python tools/r06_long_walk.py [policy] [steps]      # default policy 0, 64,000 steps (the iteration)
+    python tools/r06_long_walk.py -1 25600              # C4's shared policy, one epoch
 
 The bench configuration (4096 envs x T = 200, the test's seeds), policy `policy`: HIP walked one
 step at a time (ddrl_ppo_update_from) beside the fp64 trajectory that follows its clip outcomes,
@@ -12,26 +13,44 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 
 
+def setup_c4():
+    """C4 as tests/test_gpu_fullsize_shared.py's quarter-epoch test (4096 envs, its seeds)."""
+    from oracle import ddrl_oracle as O
+    from tests.test_gpu_fullsize_shared import C4_ENV, C4_N, _ffn_batch, _rollout
+    ctx, cfg, params, _, syn = _rollout(C4_ENV, C4_N, 13, False)
+    del syn
+    rec = ctx.records_get(0)
+    d, A = cfg.obs_dim[0], cfg.act_dim
+    batch = _ffn_batch(rec, ctx.layout[0], d, A, ctx.adv_norm_get(0))
+    sh, pe = O.sgd_schedule(np.random.default_rng(44), rec.shape[0], 128, 10)
+    return ctx, params, O.ffn_param_shapes(d, 2 * A), batch, sh, pe
+
+
 def main(q=0, steps=64000):
+    """q = Local policy q; q = -1: C4's shared policy."""
     import torch
     from oracle import ddrl_oracle as O
     from ddrl_amd.synthetic import SyntheticRollout
     from tests.gpu_harness import HipLockstep, NumpyLockstep, init_params, make_ctx, tie_following_trajectory
     from tests.test_gpu_longhorizon import N_ENVS, T, _batch
-    ctx, cfg, _ = make_ctx("QuantrupedMultiEnv_Local", N_ENVS, T)
-    params = init_params(ctx, cfg, 21, head_scale=1.0)
-    syn = SyntheticRollout(N_ENVS, T, cfg.obs_full_dim, cfg.n_agents, cfg.act_dim, "cuda:0", seed=3)
-    ctx.observe(syn.obs[0])
-    ctx.rollout_fragment(syn.obs, syn.eps, syn.fw, syn.cfrc, syn.dones_for_fragment(), syn.actions)
-    ctx.gae()
-    ctx.synchronize()
-    del syn
-    R = T * ctx.layout[0]["C"]
-    sched = [O.sgd_schedule(np.random.default_rng(40 + p), R, 128, 10) for p in range(4)]
-    A = cfg.act_dim
-    shapes = O.ffn_param_shapes(cfg.obs_dim[q], 2 * A)
-    batch = _batch(ctx.records_get(q), ctx.layout[q], cfg.obs_dim[q], A, ctx.adv_norm_get(q))
-    sh, pe = sched[q]
+    if q < 0:
+        ctx, p0, shapes, batch, sh, pe = setup_c4()
+        params, q = [p0], 0
+    else:
+        ctx, cfg, _ = make_ctx("QuantrupedMultiEnv_Local", N_ENVS, T)
+        params = init_params(ctx, cfg, 21, head_scale=1.0)
+        syn = SyntheticRollout(N_ENVS, T, cfg.obs_full_dim, cfg.n_agents, cfg.act_dim, "cuda:0", seed=3)
+        ctx.observe(syn.obs[0])
+        ctx.rollout_fragment(syn.obs, syn.eps, syn.fw, syn.cfrc, syn.dones_for_fragment(), syn.actions)
+        ctx.gae()
+        ctx.synchronize()
+        del syn
+        R = T * ctx.layout[0]["C"]
+        sched = [O.sgd_schedule(np.random.default_rng(40 + p), R, 128, 10) for p in range(4)]
+        A = cfg.act_dim
+        shapes = O.ffn_param_shapes(cfg.obs_dim[q], 2 * A)
+        batch = _batch(ctx.records_get(q), ctx.layout[q], cfg.obs_dim[q], A, ctx.adv_norm_get(q))
+        sh, pe = sched[q]
     horizons = sorted({h for h in (1600, 3200, 6400, 12800, 19200, 25600, 32000, 44800, 64000) if h <= steps} | {steps})
     t0 = time.time()
 
