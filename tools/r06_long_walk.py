@@ -3,6 +3,7 @@ one epoch, for one policy (GPU box, repo root):
 
     python tools/r06_long_walk.py [policy] [steps]      # default policy 0, 64,000 steps (the iteration)
     python tools/r06_long_walk.py -1 25600              # C4's shared policy, one epoch
+    python tools/r06_long_walk.py -2 12800              # C5's GraphNet, one epoch of one-launch steps
 
 The bench configuration (4096 envs x T = 200, the test's seeds), policy `policy`: HIP walked one
 step at a time (ddrl_ppo_update_from) beside the fp64 trajectory that follows its clip outcomes,
@@ -26,15 +27,28 @@ def setup_c4():
     return ctx, params, O.ffn_param_shapes(d, 2 * A), batch, sh, pe
 
 
+def setup_c5():
+    """C5 as tests/test_gpu_fullsize_shared.py's 1,000-step test (2048 envs, its seeds)."""
+    from oracle import ddrl_oracle as O
+    from tests.gpu_harness import GNN_ENV
+    from tests.test_gpu_fullsize_shared import C5_N, _gnn_batch, _rollout, _schedule
+    ctx, cfg, params, _, syn = _rollout(GNN_ENV, C5_N, 17, True)
+    del syn
+    rec = ctx.records_get(0)
+    sh, pe = _schedule(rec.shape[0], 8)
+    return ctx, params, O.gnn_param_shapes(4), _gnn_batch(rec, ctx.layout[0], ctx.adv_norm_get(0)), sh.numpy(), pe.numpy()
+
+
 def main(q=0, steps=64000):
-    """q = Local policy q; q = -1: C4's shared policy."""
+    """q = Local policy q; q = -1: C4's shared policy; q = -2: C5's GraphNet."""
     import torch
     from oracle import ddrl_oracle as O
     from ddrl_amd.synthetic import SyntheticRollout
     from tests.gpu_harness import HipLockstep, NumpyLockstep, init_params, make_ctx, tie_following_trajectory
     from tests.test_gpu_longhorizon import N_ENVS, T, _batch
+    model = "gnn" if q == -2 else "ffn"
     if q < 0:
-        ctx, p0, shapes, batch, sh, pe = setup_c4()
+        ctx, p0, shapes, batch, sh, pe = setup_c4() if q == -1 else setup_c5()
         params, q = [p0], 0
     else:
         ctx, cfg, _ = make_ctx("QuantrupedMultiEnv_Local", N_ENVS, T)
@@ -51,7 +65,7 @@ def main(q=0, steps=64000):
         shapes = O.ffn_param_shapes(cfg.obs_dim[q], 2 * A)
         batch = _batch(ctx.records_get(q), ctx.layout[q], cfg.obs_dim[q], A, ctx.adv_norm_get(q))
         sh, pe = sched[q]
-    horizons = sorted({h for h in (1600, 3200, 6400, 12800, 19200, 25600, 32000, 44800, 64000) if h <= steps} | {steps})
+    horizons = sorted({h for h in (100, 400, 1000, 1600, 2000, 3200, 4000, 6400, 9600, 12800, 19200, 25600, 32000, 44800, 64000) if h <= steps} | {steps})
     t0 = time.time()
 
     class Progress:
@@ -65,7 +79,7 @@ def main(q=0, steps=64000):
 
         def step(self, k):
             self.impl.step(k)
-            if (k + 1) % 2000 == 0:
+            if (k + 1) % (200 if model == "gnn" else 2000) == 0:
                 print(f"{self.tag}: step {k + 1} ({time.time() - t0:.0f} s)", flush=True)
 
         def theta(self):
@@ -74,16 +88,16 @@ def main(q=0, steps=64000):
     # past the first epoch most steps differ by more than the search threshold with no flip to
     # explain them (smooth drift): a small search keeps the walk affordable
     search = dict(pool=16, max_flips=2)
-    npl = NumpyLockstep(params[q], shapes, batch, sh, pe, 0.2)
+    npl = NumpyLockstep(params[q], shapes, batch, sh, pe, 0.2, model=model)
     m32 = []
     tf32, _, ties32 = tie_following_trajectory(None, q, params[q], shapes, batch, sh, pe, 0.2, steps, horizons,
-                                               impl=Progress(npl, "numpy"), missed=m32, **search)
+                                               impl=Progress(npl, "numpy"), missed=m32, model=model, **search)
     for h in horizons:
         print(f"numpy H={h}: |numpy fp32 - fp64 following numpy| {np.abs(npl.snaps[h] - tf32[h]).max():.3g}", flush=True)
     hip = HipLockstep(ctx, q, O.pack(params[q], shapes), sh, pe, 0.2)
     mh = []
     tf, _, ties = tie_following_trajectory(ctx, q, params[q], shapes, batch, sh, pe, 0.2, steps, horizons,
-                                           impl=Progress(hip, "HIP"), missed=mh, **search)
+                                           impl=Progress(hip, "HIP"), missed=mh, model=model, **search)
     print(f"policy {q}: flips HIP {len(ties)}, numpy {len(ties32)}; unexplained steps HIP {len(mh)} "
           f"(first {mh[0][0] if mh else '-'}), numpy {len(m32)} (first {m32[0][0] if m32 else '-'})", flush=True)
     for h in horizons:
